@@ -1,0 +1,79 @@
+"""ctypes binding of libsrbd_mpc.so (include/srbd_mpc.h).
+
+The HIP library is the only compute path: if it is missing this module raises; there is no CPU
+or PyTorch fallback for the kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from biped_pympc_amd.build import LIB_DIR
+
+_LIB_NAME = "libsrbd_mpc.so"
+_lib = None
+
+_c_dp = ctypes.c_void_p  # device pointers travel as void*
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return os.path.join(LIB_DIR, _LIB_NAME)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} not found: build it with `python -m biped_pympc_amd.build` (hipcc, gfx950). "
+            "There is no CPU fallback for the SRBD-MPC kernels.")
+    L = ctypes.CDLL(path)
+    L.srbd_abi_version.restype = ctypes.c_int
+    L.srbd_last_error.restype = ctypes.c_char_p
+    L.srbd_solver_lds_bytes.restype = ctypes.c_size_t
+    L.srbd_solver_lds_bytes.argtypes = [ctypes.c_int]
+    L.srbd_mpc_workspace_doubles.restype = ctypes.c_size_t
+    L.srbd_mpc_workspace_doubles.argtypes = [ctypes.c_int, ctypes.c_int]
+    P = ctypes.POINTER(_c_dp)
+    L.srbd_qp_former.restype = ctypes.c_int
+    L.srbd_qp_former.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_void_p]
+    L.srbd_pdipm.restype = ctypes.c_int
+    L.srbd_pdipm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_void_p]
+    L.srbd_pdipm_cold.restype = ctypes.c_int
+    L.srbd_pdipm_cold.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P,
+                                  ctypes.c_void_p]
+    L.srbd_mpc_solve.restype = ctypes.c_int
+    L.srbd_mpc_solve.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
+                                 ctypes.c_void_p, P, ctypes.c_void_p]
+    L.srbd_evaluate_qp_former.restype = ctypes.c_float
+    L.srbd_evaluate_qp_former.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int]
+    L.srbd_evaluate_pdipm.restype = ctypes.c_float
+    L.srbd_evaluate_pdipm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int]
+    L.srbd_pattern_ccs.restype = ctypes.c_int
+    L.srbd_pattern_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                   ctypes.POINTER(ctypes.c_int)]
+    _lib = L
+    return L
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr_t = _c_dp * len(ptrs)
+    return arr_t(*[int(p) if p else None for p in ptrs])
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().srbd_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed: {msg}")
+
+
+def last_error() -> str:
+    return lib().srbd_last_error().decode(errors="replace")

@@ -1,0 +1,82 @@
+"""Build the native libraries in-tree (hipcc for gfx950 + gcc for the thin CusADi-ABI shims).
+
+Outputs (biped_pympc_amd/lib/):
+  libsrbd_mpc.so                                  HIP kernels + extended C-ABI (include/srbd_mpc.h)
+  libqp_former.so                                 CusADi `evaluate` for 'qp_former' (N = 10)
+  libsparse_pdipm_multiple_iterations.so          CusADi `evaluate` for the deployed solver (N=10, 5 it)
+  libqp_former_N<N>.so, libsparse_pdipm_multiple_iterations_N<N>_K<K>.so   other configurations
+Replaces the reference's CasADi -> CUDA codegen + CMake pipeline (run_codegen.py:9-44), which
+takes ~3 h for 5 unrolled Newton iterations (README.md:80-84); this builds in seconds.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SRBD_OFFLOAD_ARCH", "gfx950")
+
+# (function name, N, K) of the thin CusADi-ABI libraries to build
+DROPIN_CONFIGS = [
+    ("qp_former", 10, None),
+    ("sparse_pdipm_multiple_iterations", 10, 5),
+    ("qp_former", 20, None),
+    ("sparse_pdipm_multiple_iterations", 10, 10),
+    ("sparse_pdipm_multiple_iterations", 20, 10),
+]
+
+
+def dropin_lib_name(fn: str, N: int, K: int | None) -> str:
+    if fn == "qp_former":
+        return "libqp_former.so" if N == 10 else f"libqp_former_N{N}.so"
+    if N == 10 and K == 5:
+        return "libsparse_pdipm_multiple_iterations.so"
+    return f"libsparse_pdipm_multiple_iterations_N{N}_K{K}.so"
+
+
+def _newer(target: str, sources: list[str]) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(s) <= t for s in sources)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    core = os.path.join(LIB_DIR, "libsrbd_mpc.so")
+    srcs = [os.path.join(CSRC, f) for f in
+            ("srbd_mpc.hip", "srbd_common.hpp", "pdipm.hpp", "qp_former.hpp")]
+    srcs.append(os.path.join(INCLUDE, "srbd_mpc.h"))
+    if force or not _newer(core, srcs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-o", core, os.path.join(CSRC, "srbd_mpc.hip")]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    shim = os.path.join(CSRC, "dropin_evaluate.c")
+    for fn, N, K in DROPIN_CONFIGS:
+        out = os.path.join(LIB_DIR, dropin_lib_name(fn, N, K))
+        if not force and _newer(out, [shim, core, os.path.join(INCLUDE, "srbd_mpc.h")]):
+            continue
+        defs = ["-DSRBD_FN_FORMER"] if fn == "qp_former" else ["-DSRBD_FN_PDIPM", f"-DSRBD_ITERS={K}"]
+        cmd = ["gcc", "-O2", "-fPIC", "-shared", f"-DSRBD_N={N}", *defs, "-o", out, shim,
+               f"-L{LIB_DIR}", "-lsrbd_mpc", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+    return core
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

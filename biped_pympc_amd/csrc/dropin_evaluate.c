@@ -1,0 +1,21 @@
+/* dropin_evaluate.c -- thin CusADi-ABI library: exports exactly `evaluate`, the symbol a CusADi
+ * function library exports (reference biped_pympc/cusadi/src/generateCUDACode.py:157-183) and that
+ * CusadiFunction binds (CusadiFunction.py:34-35,43-46). Compiled once per CasADi Function name:
+ *   -DSRBD_FN_FORMER -DSRBD_N=10                 -> libqp_former.so
+ *   -DSRBD_FN_PDIPM  -DSRBD_N=10 -DSRBD_ITERS=5  -> libsparse_pdipm_multiple_iterations.so
+ * and forwards to libsrbd_mpc.so (same directory, rpath $ORIGIN). */
+#include "../../include/srbd_mpc.h"
+
+#ifndef SRBD_N
+#define SRBD_N 10
+#endif
+
+float evaluate(const double* inputs[], double* work, double* outputs[], const int batch_size) {
+#if defined(SRBD_FN_FORMER)
+  return srbd_evaluate_qp_former(SRBD_N, inputs, work, outputs, batch_size);
+#elif defined(SRBD_FN_PDIPM)
+  return srbd_evaluate_pdipm(SRBD_N, SRBD_ITERS, inputs, work, outputs, batch_size);
+#else
+#error "define SRBD_FN_FORMER or SRBD_FN_PDIPM"
+#endif
+}

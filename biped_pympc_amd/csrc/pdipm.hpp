@@ -1,0 +1,617 @@
+// pdipm.hpp -- HIP kernel for the batched Mehrotra primal-dual interior-point Newton loop.
+//
+// Replaces the CusADi-generated kernel of CasADi Function 'sparse_pdipm_multiple_iterations'
+// (reference biped_pympc/casadi/sparse_pdipm_solver.py:357-534), same 10 inputs / 6 outputs and
+// the same batched row layout, but with the Newton-iteration count a RUNTIME argument (the
+// reference bakes 5 iterations into a ~3 h compile, README.md:80-84).
+//
+// Per iteration the reference factorises the full 70N x 70N quasi-definite KKT
+//   [[H+bI, 0, G^T, A^T], [0, S^-1Z+dI, I, 0], [G, I, -dI, 0], [A, 0, 0, -dI]]
+// with a sparse LDL^T and solves it twice (affine + corrector). This kernel solves the SAME linear
+// systems by exact block elimination, exploiting the stage structure:
+//   W = S^-1 Z + dI, D = I + dW, Lam = D^-1 W            (diagonal)
+//   dz = D^-1 (r2 - W r3) + Lam G dx,   ds = r3 - G dx + d dz
+//   [[Phi, A^T], [A, -dI]] [dx; dy] = [r1 - G^T D^-1 (r2 - W r3); r4],  Phi = H + bI + G^T Lam G
+// Phi is block diagonal per stage (x: diagonal; u: two 4x4 foot blocks + 4 scalars). The two
+// x-moment rows per stage pair with the decoupled u_i[6], u_i[9] and are eliminated as exact 2x2
+// blocks, leaving the dual system (A_dyn Phi^-1 A_dyn^T + dI) dy = g, which is block-tridiagonal
+// with 12x12 SPD blocks. It is factored by a block recursion D_i = S_ii - S_{i,i-1} D_{i-1}^-1
+// S_{i,i-1}^T keeping explicit D_i^-1 (symmetric sweep), and the corrector reuses the factors
+// (as the reference reuses its LDL, :482). Affine and corrector right-hand sides are combined
+// into one solve (linear, so identical in exact arithmetic).
+//
+// Mapping (gfx950): one wavefront per QP; the QP's CCS values (H, G, A), its iterate and all
+// factors live in LDS for the whole solve (loaded once, coalesced); f, h, b are re-read from
+// global each iteration (L2-resident). Stage-parallel work (residuals, Phi blocks, the N
+// diagonal dual blocks) is spread over the 64 lanes; the stage recursion is sequential.
+#pragma once
+#include "srbd_common.hpp"
+
+namespace srbd {
+
+struct SolverArgs {
+  const double* in[10];  // Q_val, G_val, A_val, f, h, b, x, s, z, y
+  double* out[6];        // x, s, z, y, residuals(4), mu(1)
+  const double* const* dev_in;
+  double* const* dev_out;
+  int N;
+  int n_iter;
+  int batch;
+  int init_mode;  // 0: iterate from inputs 6..9; 1: x=0, s=max(h,1), z=1, y=y0 (GPU caller init)
+  double y0;
+};
+
+__device__ inline const double* solver_in(const SolverArgs& a, int i) {
+  return a.dev_in ? a.dev_in[i] : a.in[i];
+}
+__device__ inline double* solver_out(const SolverArgs& a, int i) {
+  return a.dev_out ? a.dev_out[i] : a.out[i];
+}
+
+// LDS carve (doubles) for horizon N; every offset is a multiple of 2 doubles (16 B).
+struct SolverLayout {
+  int AV, GV, HV, X, S, Z, Y, RX, RS, RE, SI, WD, DI, R2, VV, PH, DV, R1T, TV, QV, WV, DS, DZ, DY, SC,
+      total;
+  __host__ __device__ SolverLayout(int N) {
+    const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
+    int o = 0;
+    auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
+    AV = take(122 * N - 24); GV = take(28 * N); HV = take(nz);
+    X = take(nz); S = take(m); Z = take(m); Y = take(p);
+    RX = take(nz); RS = take(m); RE = take(p);
+    SI = take(m); WD = take(m); DI = take(m); R2 = take(m); VV = take(m);
+    PH = take(24 * N); DV = take(78 * N);
+    R1T = take(nz); TV = take(nz);
+    QV = take(nd); WV = take(nd);
+    DS = take(m); DZ = take(m); DY = take(p);
+    SC = take(160);
+    total = o;
+  }
+};
+
+__device__ inline int sym_idx(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
+
+// Symmetric sweep of a small SPD matrix held in registers (packed lower) -> its inverse.
+template <int n>
+__device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    const double id = 1.0 / a[k * (k + 1) / 2 + k];
+    double col[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) col[i] = a[sym_idx(i, k)];
+#pragma unroll
+    for (int r = 0; r < n; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c) {
+        const int e = r * (r + 1) / 2 + c;
+        if (r != k && c != k) a[e] = a[e] - col[r] * col[c] * id;
+        else if (r == k && c == k) a[e] = -id;
+        else a[e] = a[e] * id;
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < n * (n + 1) / 2; ++e) a[e] = -a[e];
+}
+
+struct SolverCtx {
+  int N, nz, m, p, nd, lane;
+  double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,
+      *QV, *WV, *DS, *DZ, *DY, *SC;
+  const double *fg, *hg, *bg;
+
+  // ---- structured access to the CCS values (stage-periodic tables) ----
+  __device__ double Pv(int i, int r) const { return AV[a_pidx(c_tab, N, i, r)]; }
+  __device__ double Mv(int i, int r, int j) const {  // stage i rows x x_i columns, i >= 1
+    const int o = c_tab.Mi[r][j];
+    return o >= 0 ? AV[a_xblock(i) + o] : 0.0;
+  }
+  __device__ double Nv(int i, int r, int j) const {
+    const int o = c_tab.Ni[r][j];
+    return o >= 0 ? AV[a_ublock(N, i) + o] : 0.0;
+  }
+  __device__ double E6(int i) const { return AV[a_ublock(N, i) + c_tab.e6]; }
+  __device__ double E9(int i) const { return AV[a_ublock(N, i) + c_tab.e9]; }
+  __device__ double phix(int k, int j) const { return HV[12 * (k - 1) + j] + kBeta; }  // x_k, k >= 1
+  __device__ double phiu(int i, int j) const { return HV[12 * N + 12 * i + j] + kBeta; }
+  // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i)
+  __device__ double Ssub(int i, int r, int c) const {
+    const int o = c_tab.Mi[r][c];
+    return o >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, c) / phix(i, c) : 0.0;
+  }
+  __device__ double G(int i, int q) const { return GV[28 * i + q]; }
+
+  // ---------------------------------------------------------------------- residuals ----
+  // rx = Qx + f + G^T z + A^T y ; re = A x - b ; rs = G x + s - h ; returns mu = s'z/m
+  __device__ double residuals() {
+    for (int c = lane; c < nz; c += 64) {
+      double v = HV[c] * X[c] + fg[c];
+      if (c >= 12 * N) {
+        const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
+        double gz = 0.0;
+        for (int q = 0; q < 28; ++q)
+          if (c_tab.gcol[q] == j) gz += G(i, q) * Z[16 * i + c_tab.grow[q]];
+        double ay = 0.0;
+        const int ub = a_ublock(N, i) + c_tab.cpu[j];
+        for (int t = 0; t < c_tab.su_n[j]; ++t) ay += AV[ub + t] * Y[12 * i + c_tab.su[j][t]];
+        if (j == 6) ay += AV[ub + c_tab.su_n[j]] * Y[12 * N + 2 * i];
+        if (j == 9) ay += AV[ub + c_tab.su_n[j]] * Y[12 * N + 2 * i + 1];
+        v = (v + gz) + ay;
+      } else {
+        const int k = c / 12 + 1, j = c % 12;
+        double ay;
+        if (k < N) {
+          const int xb = a_xblock(k) + c_tab.cpx[j];
+          ay = AV[xb] * Y[12 * (k - 1) + j];
+          for (int t = 0; t < c_tab.sx_n[j]; ++t) ay += AV[xb + 1 + t] * Y[12 * k + c_tab.sx[j][t]];
+        } else {
+          ay = AV[36 * (N - 1) + j] * Y[12 * (k - 1) + j];
+        }
+        v = v + ay;
+      }
+      RX[c] = v;
+    }
+    for (int e = lane; e < p; e += 64) {
+      double v = 0.0;
+      if (e < 12 * N) {
+        const int i = e / 12, r = e % 12;
+        if (i >= 1)
+          for (int j = 0; j < 12; ++j) {
+            const int o = c_tab.Mi[r][j];
+            if (o >= 0) v += AV[a_xblock(i) + o] * X[12 * (i - 1) + j];
+          }
+        v += Pv(i, r) * X[12 * i + r];
+        for (int j = 0; j < 12; ++j) {
+          const int o = c_tab.Ni[r][j];
+          if (o >= 0) v += AV[a_ublock(N, i) + o] * X[12 * N + 12 * i + j];
+        }
+      } else {
+        const int i = (e - 12 * N) / 2, w = (e - 12 * N) % 2;
+        v = (w == 0 ? E6(i) * X[12 * N + 12 * i + 6] : E9(i) * X[12 * N + 12 * i + 9]);
+      }
+      RE[e] = v - bg[e];
+    }
+    double sz = 0.0;
+    for (int q = lane; q < m; q += 64) {
+      const int i = q / 16, k = q % 16;
+      double v = 0.0;
+      for (int t = 0; t < c_tab.gr_n[k]; ++t)
+        v += G(i, c_tab.gr_off[k][t]) * X[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      RS[q] = (v + S[q]) - hg[q];
+      sz += S[q] * Z[q];
+    }
+    __syncthreads();
+    return wave_sum(sz) / m;
+  }
+
+  // ---------------------------------------------------------------------- factorise ----
+  __device__ void factor() {
+    for (int q = lane; q < m; q += 64) {
+      const double si = 1.0 / S[q];
+      const double w = si * Z[q] + kDelta;  // S^-1 Z + delta I (sparse_pdipm_solver.py:427)
+      SI[q] = si;
+      WD[q] = w;
+      DI[q] = 1.0 / (1.0 + kDelta * w);
+    }
+    __syncthreads();
+    // Phi_u foot blocks (lane per (stage, foot)) and decoupled scalars (lane per stage)
+    for (int task = lane; task < 3 * N; task += 64) {
+      if (task < 2 * N) {
+      const int i = task >> 1, f = task & 1;
+      double a[10];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? phiu(i, c_tab.foot_col[f][r]) : 0.0;
+      for (int k = 0; k < 8; ++k) {
+        const int q = 16 * i + 8 * f + k;
+        const double lam = DI[q] * WD[q];
+        double g4[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int t = 0; t < c_tab.gr_n[8 * f + k]; ++t)
+          g4[c_tab.col_pos[c_tab.gr_col[8 * f + k][t]]] = G(i, c_tab.gr_off[8 * f + k][t]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
+      }
+      sweep_inverse<4>(a);
+#pragma unroll
+      for (int e = 0; e < 10; ++e) PH[24 * i + 10 * f + e] = a[e];
+      } else {
+      const int i = task - 2 * N;
+      const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);
+      PH[24 * i + 20] = kDelta / (p6 * kDelta + e6 * e6);  // gamma_6 (exact 2x2 elimination)
+      PH[24 * i + 21] = kDelta / (p9 * kDelta + e9 * e9);
+      PH[24 * i + 22] = 1.0 / phiu(i, 8);
+      PH[24 * i + 23] = 1.0 / phiu(i, 11);
+      }
+    }
+    __syncthreads();
+    // diagonal dual blocks S_ii (all stages in parallel), packed lower 78 per stage
+    for (int e = lane; e < 78 * N; e += 64) {
+      const int i = e / 78, l = e % 78;
+      int r = 0;
+      while ((r + 1) * (r + 2) / 2 <= l) ++r;
+      const int c = l - r * (r + 1) / 2;
+      double v = 0.0;
+      if (r == c) {
+        const double pr = Pv(i, r);
+        v = pr * pr / phix(i + 1, r) + kDelta;
+      }
+      if (i >= 1)
+        for (int j = 0; j < 12; ++j) {
+          const int o1 = c_tab.Mi[r][j], o2 = c_tab.Mi[c][j];
+          if (o1 >= 0 && o2 >= 0) v += AV[a_xblock(i) + o1] * AV[a_xblock(i) + o2] / phix(i, j);
+        }
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        double vr[4], vc[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          vr[a] = Nv(i, r, c_tab.foot_col[f][a]);
+          vc[a] = Nv(i, c, c_tab.foot_col[f][a]);
+        }
+        const double* ph = PH + 24 * i + 10 * f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * vc[b];
+          v += vr[a] * t;
+        }
+      }
+      v += Nv(i, r, 6) * Nv(i, c, 6) * PH[24 * i + 20] + Nv(i, r, 9) * Nv(i, c, 9) * PH[24 * i + 21] +
+           Nv(i, r, 8) * Nv(i, c, 8) * PH[24 * i + 22] + Nv(i, r, 11) * Nv(i, c, 11) * PH[24 * i + 23];
+      DV[e] = v;
+    }
+    __syncthreads();
+    // block recursion over stages: D_i = S_ii - S_{i,i-1} D_{i-1}^-1 S_{i,i-1}^T ; DV_i <- D_i^-1
+    for (int i = 0; i < N; ++i) {
+      double* Di = DV + 78 * i;
+      if (i >= 1) {
+        const double* Dp = DV + 78 * (i - 1);
+        for (int e = lane; e < 144; e += 64) {
+          const int r = e / 12, c = e % 12;
+          double u = 0.0;
+          for (int k = 0; k < 12; ++k) {
+            const int o = c_tab.Mi[r][k];
+            if (o >= 0) u += Ssub(i, r, k) * Dp[sym_idx(k, c)];
+          }
+          SC[e] = u;
+        }
+        __syncthreads();
+        for (int e = lane; e < 78; e += 64) {
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= e) ++r;
+          const int c = e - r * (r + 1) / 2;
+          double acc = 0.0;
+          for (int k = 0; k < 12; ++k)
+            if (c_tab.Mi[c][k] >= 0) acc += SC[r * 12 + k] * Ssub(i, c, k);
+          Di[e] -= acc;
+        }
+        __syncthreads();
+      }
+      // in-place symmetric sweep of the 12x12 block (78 packed entries over 64 lanes)
+      int r0 = 0, r1 = 0;
+      const int e0 = lane, e1 = lane + 64;
+      while ((r0 + 1) * (r0 + 2) / 2 <= e0) ++r0;
+      if (e1 < 78)
+        while ((r1 + 1) * (r1 + 2) / 2 <= e1) ++r1;
+      const int c0 = e0 - r0 * (r0 + 1) / 2, c1 = e1 - r1 * (r1 + 1) / 2;
+      for (int k = 0; k < 12; ++k) {
+        const double id = 1.0 / Di[k * (k + 1) / 2 + k];
+        const double a0 = Di[e0], k0r = Di[sym_idx(r0, k)], k0c = Di[sym_idx(c0, k)];
+        double a1 = 0.0, k1r = 0.0, k1c = 0.0;
+        if (e1 < 78) { a1 = Di[e1]; k1r = Di[sym_idx(r1, k)]; k1c = Di[sym_idx(c1, k)]; }
+        __syncthreads();
+        double n0, n1 = 0.0;
+        if (r0 != k && c0 != k) n0 = a0 - k0r * k0c * id;
+        else if (r0 == k && c0 == k) n0 = -id;
+        else n0 = a0 * id;
+        if (e1 < 78) {
+          if (r1 != k && c1 != k) n1 = a1 - k1r * k1c * id;
+          else if (r1 == k && c1 == k) n1 = -id;
+          else n1 = a1 * id;
+        }
+        Di[e0] = n0;
+        if (e1 < 78) Di[e1] = n1;
+        __syncthreads();
+      }
+      Di[e0] = -Di[e0];
+      if (e1 < 78) Di[e1] = -Di[e1];
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------------------- solve ----
+  // Solves K [dx; ds; dz; dy] = [-RX; R2; -RS; -RE] with the current factors.
+  // Result: dx -> TV, ds -> DS, dz -> DZ, dy -> DY.
+  __device__ void solve() {
+    for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
+    __syncthreads();
+    // r1~ = r1 - G^T VV
+    for (int c = lane; c < nz; c += 64) {
+      double v = -RX[c];
+      if (c >= 12 * N) {
+        const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
+        double g = 0.0;
+        for (int q = 0; q < 28; ++q)
+          if (c_tab.gcol[q] == j) g += G(i, q) * VV[16 * i + c_tab.grow[q]];
+        v -= g;
+      }
+      R1T[c] = v;
+    }
+    __syncthreads();
+    // t = Phi^-1 r1~ (x: diagonal; u: foot blocks, scalars, x-moment pairs)
+    for (int c = lane; c < 12 * N; c += 64) TV[c] = R1T[c] / phix(c / 12 + 1, c % 12);
+    for (int task = lane; task < 3 * N; task += 64) {
+      if (task < 2 * N) {
+      const int i = task >> 1, f = task & 1;
+      const double* ph = PH + 24 * i + 10 * f;
+      double rv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) rv[a] = R1T[12 * N + 12 * i + c_tab.foot_col[f][a]];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * rv[b];
+        TV[12 * N + 12 * i + c_tab.foot_col[f][a]] = t;
+      }
+      } else {
+      const int i = task - 2 * N;
+      const int b = 12 * N + 12 * i;
+      const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);
+      const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
+      TV[b + 6] = (kDelta * R1T[b + 6] + e6 * r4a) / (p6 * kDelta + e6 * e6);
+      TV[b + 9] = (kDelta * R1T[b + 9] + e9 * r4b) / (p9 * kDelta + e9 * e9);
+      TV[b + 8] = R1T[b + 8] * PH[24 * i + 22];
+      TV[b + 11] = R1T[b + 11] * PH[24 * i + 23];
+      }
+    }
+    __syncthreads();
+    // g = A_dyn t - r4_dyn
+    for (int e = lane; e < 12 * N; e += 64) {
+      const int i = e / 12, r = e % 12;
+      double v = 0.0;
+      if (i >= 1)
+        for (int j = 0; j < 12; ++j) {
+          const int o = c_tab.Mi[r][j];
+          if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
+        }
+      v += Pv(i, r) * TV[12 * i + r];
+      for (int j = 0; j < 12; ++j) {
+        const int o = c_tab.Ni[r][j];
+        if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
+      }
+      QV[e] = v + RE[e];
+    }
+    __syncthreads();
+    // forward: q_i -= S_{i,i-1} w_{i-1} ; w_i = D_i^-1 q_i
+    for (int i = 0; i < N; ++i) {
+      if (i >= 1) {
+        if (lane < 12) {
+          double acc = 0.0;
+          for (int k = 0; k < 12; ++k)
+            if (c_tab.Mi[lane][k] >= 0) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
+          QV[12 * i + lane] -= acc;
+        }
+        __syncthreads();
+      }
+      if (lane < 12) {
+        const double* Di = DV + 78 * i;
+        double acc = 0.0;
+        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * QV[12 * i + k];
+        WV[12 * i + lane] = acc;
+      }
+      __syncthreads();
+    }
+    // backward: y_{N-1} = w_{N-1} ; y_i = w_i - D_i^-1 S_{i+1,i}^T y_{i+1}   (y stored in QV)
+    if (lane < 12) QV[12 * (N - 1) + lane] = WV[12 * (N - 1) + lane];
+    __syncthreads();
+    for (int i = N - 2; i >= 0; --i) {
+      if (lane < 12) {
+        double acc = 0.0;
+        for (int r = 0; r < 12; ++r)
+          if (c_tab.Mi[r][lane] >= 0) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
+        SC[lane] = acc;
+      }
+      __syncthreads();
+      if (lane < 12) {
+        const double* Di = DV + 78 * i;
+        double acc = 0.0;
+        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * SC[k];
+        QV[12 * i + lane] = WV[12 * i + lane] - acc;
+      }
+      __syncthreads();
+    }
+    // dx = t - Phi^-1 A_dyn^T dy ; x-moment duals from the exact 2x2 elimination
+    for (int c = lane; c < 12 * N; c += 64) {
+      const int k = c / 12 + 1, j = c % 12;
+      double aty;
+      if (k < N) {
+        const int xb = a_xblock(k) + c_tab.cpx[j];
+        aty = AV[xb] * QV[12 * (k - 1) + j];
+        for (int t = 0; t < c_tab.sx_n[j]; ++t) aty += AV[xb + 1 + t] * QV[12 * k + c_tab.sx[j][t]];
+      } else {
+        aty = AV[36 * (N - 1) + j] * QV[12 * (k - 1) + j];
+      }
+      TV[c] = TV[c] - aty / phix(k, j);
+    }
+    for (int task = lane; task < 3 * N; task += 64) {
+      // u columns: per (stage, foot) block or per stage scalars
+      const bool foot = task < 2 * N;
+      const int i = foot ? (task >> 1) : task - 2 * N;
+      const int b = 12 * N + 12 * i;
+      auto aty_u = [&](int j) {
+        const int ub = a_ublock(N, i) + c_tab.cpu[j];
+        double a = 0.0;
+        for (int t = 0; t < c_tab.su_n[j]; ++t) a += AV[ub + t] * QV[12 * i + c_tab.su[j][t]];
+        return a;
+      };
+      if (foot) {
+        const int f = task & 1;
+        const double* ph = PH + 24 * i + 10 * f;
+        double av[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) av[a] = aty_u(c_tab.foot_col[f][a]);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
+          TV[b + c_tab.foot_col[f][a]] -= t;
+        }
+      } else {
+        const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);
+        const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
+        const double a6 = aty_u(6), a9 = aty_u(9), a8 = aty_u(8), a11 = aty_u(11);
+        TV[b + 6] -= PH[24 * i + 20] * a6;
+        TV[b + 9] -= PH[24 * i + 21] * a9;
+        TV[b + 8] -= PH[24 * i + 22] * a8;
+        TV[b + 11] -= PH[24 * i + 23] * a11;
+        const double rho6 = R1T[b + 6] - a6, rho9 = R1T[b + 9] - a9;
+        DY[12 * N + 2 * i] = (e6 * rho6 - p6 * r4a) / (p6 * kDelta + e6 * e6);
+        DY[12 * N + 2 * i + 1] = (e9 * rho9 - p9 * r4b) / (p9 * kDelta + e9 * e9);
+      }
+    }
+    for (int e = lane; e < 12 * N; e += 64) DY[e] = QV[e];
+    __syncthreads();
+    // dz = D^-1 (r2 - W r3) + Lam G dx ; ds = r3 - G dx + delta dz
+    for (int q = lane; q < m; q += 64) {
+      const int i = q / 16, k = q % 16;
+      double gd = 0.0;
+      for (int t = 0; t < c_tab.gr_n[k]; ++t)
+        gd += G(i, c_tab.gr_off[k][t]) * TV[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      const double dz = VV[q] + DI[q] * WD[q] * gd;
+      DZ[q] = dz;
+      DS[q] = -RS[q] - gd + kDelta * dz;
+    }
+    __syncthreads();
+  }
+
+  // fmax(fmin(1, 0.99 * min_i if_else(dv_i < 0, -v_i/dv_i, 1)), 1e-12)  (:460-467)
+  __device__ double step_length(const double* v, const double* dv) const {
+    double mn = INFINITY;
+    for (int q = lane; q < m; q += 64) {
+      const bool c = dv[q] < 0.0;
+      const double a = -v[q] / dv[q];
+      const double cand = (c ? a : 0.0) + (!c ? 1.0 : 0.0);
+      mn = fmin(mn, cand);
+    }
+    mn = wave_min(mn);
+    return fmax(fmin(1.0, 0.99 * mn), 1e-12);
+  }
+};
+
+__global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int env = blockIdx.x;
+  if (env >= args.batch) return;
+  const int N = args.N;
+  const SolverLayout Lo(N);
+  SolverCtx C;
+  C.N = N;
+  C.nz = 24 * N;
+  C.m = 16 * N;
+  C.p = 14 * N;
+  C.nd = 12 * N;
+  C.lane = threadIdx.x;
+  C.AV = smem + Lo.AV; C.GV = smem + Lo.GV; C.HV = smem + Lo.HV;
+  C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
+  C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE;
+  C.SI = smem + Lo.SI; C.WD = smem + Lo.WD; C.DI = smem + Lo.DI; C.R2 = smem + Lo.R2; C.VV = smem + Lo.VV;
+  C.PH = smem + Lo.PH; C.DV = smem + Lo.DV; C.R1T = smem + Lo.R1T; C.TV = smem + Lo.TV;
+  C.QV = smem + Lo.QV; C.WV = smem + Lo.WV; C.DS = smem + Lo.DS; C.DZ = smem + Lo.DZ; C.DY = smem + Lo.DY;
+  C.SC = smem + Lo.SC;
+  const int lane = C.lane, nz = C.nz, m = C.m, p = C.p;
+  const int nA = nnz_A(N), nG = 28 * N;
+  const double* Hg = solver_in(args, 0) + (size_t)env * nz;
+  const double* Gg = solver_in(args, 1) + (size_t)env * nG;
+  const double* Ag = solver_in(args, 2) + (size_t)env * nA;
+  C.fg = solver_in(args, 3) + (size_t)env * nz;
+  C.hg = solver_in(args, 4) + (size_t)env * m;
+  C.bg = solver_in(args, 5) + (size_t)env * p;
+  for (int e = lane; e < nA; e += 64) C.AV[e] = Ag[e];
+  for (int e = lane; e < nG; e += 64) C.GV[e] = Gg[e];
+  for (int e = lane; e < nz; e += 64) C.HV[e] = Hg[e];
+  if (args.init_mode == 0) {
+    const double* xg = solver_in(args, 6) + (size_t)env * nz;
+    const double* sg = solver_in(args, 7) + (size_t)env * m;
+    const double* zg = solver_in(args, 8) + (size_t)env * m;
+    const double* yg = solver_in(args, 9) + (size_t)env * p;
+    for (int e = lane; e < nz; e += 64) C.X[e] = xg[e];
+    for (int e = lane; e < m; e += 64) { C.S[e] = sg[e]; C.Z[e] = zg[e]; }
+    for (int e = lane; e < p; e += 64) C.Y[e] = yg[e];
+  } else {
+    // mpc_controller_cusadi.py:138-141: x = 0, s = max(d - G 0, 1), z = 1, y = y0
+    for (int e = lane; e < nz; e += 64) C.X[e] = 0.0;
+    for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - 0.0, 1.0); C.Z[e] = 1.0; }
+    for (int e = lane; e < p; e += 64) C.Y[e] = args.y0;
+  }
+  __syncthreads();
+
+  double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
+  for (int it = 0; it < args.n_iter; ++it) {
+    const double mu = C.residuals();
+    C.factor();
+    // affine: r2 = -(S^-1 (s o z))
+    for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
+    __syncthreads();
+    C.solve();
+    const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
+    double sza = 0.0;
+    for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
+    const double mu_aff = wave_sum(sza) / m;
+    const double sigma = pow(mu_aff / mu, 3.0);
+    // combined rhs: r2 = -(S^-1 (s o z)) - S^-1 (s o z + ds_a o dz_a - sigma mu e)
+    __syncthreads();
+    for (int q = lane; q < m; q += 64) {
+      const double rc = C.S[q] * C.Z[q] + C.DS[q] * C.DZ[q] - sigma * mu * 1.0;
+      C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q])) + -(C.SI[q] * rc);
+    }
+    __syncthreads();
+    C.solve();
+    const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
+    __syncthreads();
+    double szn = 0.0;
+    for (int e = lane; e < nz; e += 64) C.X[e] = C.X[e] + apc * C.TV[e];
+    for (int q = lane; q < m; q += 64) {
+      const double sn = fmax(C.S[q] + apc * C.DS[q], 1e-8);
+      const double zn = fmax(fmax(C.Z[q] + adc * C.DZ[q], 1e-8), 1e-8);
+      C.S[q] = sn;
+      C.Z[q] = zn;
+      szn += sn * zn;
+    }
+    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * C.DY[e];
+    mu_new = wave_sum(szn) / m;
+    if (it == args.n_iter - 1) {
+      double a = 0.0, b = 0.0, c = 0.0;
+      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
+      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
+      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
+      res0 = sqrt(wave_sum(a));
+      res1 = sqrt(wave_sum(b));
+      res2 = sqrt(wave_sum(c));
+    }
+    __syncthreads();
+  }
+  double* xo = solver_out(args, 0) + (size_t)env * nz;
+  double* so = solver_out(args, 1) + (size_t)env * m;
+  double* zo = solver_out(args, 2) + (size_t)env * m;
+  double* yo = solver_out(args, 3) + (size_t)env * p;
+  double* ro = solver_out(args, 4) + (size_t)env * 4;
+  double* mo = solver_out(args, 5) + (size_t)env;
+  for (int e = lane; e < nz; e += 64) xo[e] = C.X[e];
+  for (int e = lane; e < m; e += 64) { so[e] = C.S[e]; zo[e] = C.Z[e]; }
+  for (int e = lane; e < p; e += 64) yo[e] = C.Y[e];
+  if (lane == 0) {
+    ro[0] = res0;
+    ro[1] = res1;
+    ro[2] = res2;
+    ro[3] = mu_new;
+    mo[0] = mu_new;
+  }
+}
+
+}  // namespace srbd

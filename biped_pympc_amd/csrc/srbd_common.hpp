@@ -1,0 +1,170 @@
+// srbd_common.hpp -- shared definitions for the SRBD-MPC HIP kernels (gfx950 / CDNA4, wave64).
+//
+// Stage-periodic sparsity tables of the QP produced by qp_former (reference
+// biped_pympc/casadi/srbd_constraints.py:83-227; CCS convention sparse_pdipm_solver.py:561-591).
+// The same closed-form rules live in biped_pympc_amd/layout.py; tests/test_layout.py checks that
+// both agree with a structural dependency analysis of the literal RK4 model.
+//
+// Decision vector z = [x_1..x_N, u_0..u_{N-1}];  x_k[j] -> 12(k-1)+j,  u_i[j] -> 12N+12i+j.
+// Rows: dynamics of stage i -> 12i+r ; x-moment rows -> 12N+2i+{0,1} ; inequalities -> 16i+8f+k.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srbd {
+
+constexpr double kBeta = 1e-8;    // generate_solver_function.py:112
+constexpr double kDelta = 1e-8;   // sparse_pdipm_solver.py:416
+constexpr double kFMax = 500.0;   // srbd_constraints.py:31
+constexpr double kLt = 0.07;      // srbd_constraints.py:161
+constexpr double kLh = 0.04;      // srbd_constraints.py:162
+constexpr double kGravZ = -9.81;  // srbd_centroidal_model.py:136
+constexpr int kMaxN = 32;         // horizon supported by the kernels (LDS-bound)
+
+struct Tables {
+  // S_x(j): stage-local rows touched by x_i[j] through -A_d (count sx_n[j], rows sx[j][t]).
+  int8_t sx_n[12];
+  int8_t sx[12][4];
+  // S_u(j): stage-local rows touched by u_i[j] through -B_d.
+  int8_t su_n[12];
+  int8_t su[12][8];
+  // CCS column offsets inside one periodic block (x block = 36 values, u block = 86 values).
+  int16_t cpx[12];  // start of column x_k[j] inside the 36-value block of x_k (k < N)
+  int16_t cpu[12];  // start of column u_i[j] inside the 86-value block of u_i
+  int16_t e6, e9;   // x-moment entries (rows 12N+2i, 12N+2i+1) inside the u_i block
+  // Dense 12x12 stage-local index maps into the periodic blocks (-1 = structural zero):
+  //   Mi[r][j]: entry of M_i = (stage i rows, x_i columns)  -> offset inside x_i's 36-block
+  //   Ni[r][j]: entry of N_i = (stage i rows, u_i columns)  -> offset inside u_i's 86-block
+  int16_t Mi[12][12];
+  int16_t Ni[12][12];
+  // G: 28 values per stage in CCS order; gcol/grow give the (u column, stage-local row) pair.
+  int8_t gcol[28];
+  int8_t grow[28];
+  // Row-wise view of G: row k (0..15) -> up to 2 entries (value offset, u column).
+  int8_t gr_n[16];
+  int8_t gr_off[16][2];
+  int8_t gr_col[16][2];
+  // Foot blocks of Phi_u: u columns {0,1,2,7} (left) and {3,4,5,10} (right).
+  int8_t foot_col[2][4];
+  // column -> (foot, position) or -1 for the four decoupled columns {6,8,9,11}
+  int8_t col_foot[12];
+  int8_t col_pos[12];
+};
+
+constexpr Tables make_tables() {
+  Tables t{};
+  for (int j = 0; j < 12; ++j) {
+    if (j <= 5) {
+      t.sx_n[j] = 1;
+      t.sx[j][0] = (int8_t)j;
+    } else if (j <= 8) {
+      t.sx_n[j] = 4;
+      t.sx[j][0] = 0; t.sx[j][1] = 1; t.sx[j][2] = 2; t.sx[j][3] = (int8_t)j;
+    } else {
+      t.sx_n[j] = 2;
+      t.sx[j][0] = (int8_t)(j - 6); t.sx[j][1] = (int8_t)j;
+    }
+    if (j <= 2) {
+      const int8_t r[8] = {0, 1, 2, (int8_t)(3 + j), 6, 7, 8, (int8_t)(9 + j)};
+      t.su_n[j] = 8;
+      for (int q = 0; q < 8; ++q) t.su[j][q] = r[q];
+    } else if (j <= 5) {
+      const int8_t r[8] = {0, 1, 2, (int8_t)j, 6, 7, 8, (int8_t)(6 + j)};
+      t.su_n[j] = 8;
+      for (int q = 0; q < 8; ++q) t.su[j][q] = r[q];
+    } else {
+      const int8_t r[6] = {0, 1, 2, 6, 7, 8};
+      t.su_n[j] = 6;
+      for (int q = 0; q < 6; ++q) t.su[j][q] = r[q];
+    }
+  }
+  int acc = 0;
+  for (int j = 0; j < 12; ++j) {
+    t.cpx[j] = (int16_t)acc;
+    acc += 1 + t.sx_n[j];
+  }
+  acc = 0;
+  for (int j = 0; j < 12; ++j) {
+    t.cpu[j] = (int16_t)acc;
+    acc += t.su_n[j] + ((j == 6 || j == 9) ? 1 : 0);
+  }
+  t.e6 = (int16_t)(t.cpu[6] + t.su_n[6]);
+  t.e9 = (int16_t)(t.cpu[9] + t.su_n[9]);
+  for (int r = 0; r < 12; ++r)
+    for (int j = 0; j < 12; ++j) {
+      t.Mi[r][j] = -1;
+      t.Ni[r][j] = -1;
+    }
+  for (int j = 0; j < 12; ++j) {
+    for (int q = 0; q < t.sx_n[j]; ++q) t.Mi[t.sx[j][q]][j] = (int16_t)(t.cpx[j] + 1 + q);
+    for (int q = 0; q < t.su_n[j]; ++q) t.Ni[t.su[j][q]][j] = (int16_t)(t.cpu[j] + q);
+  }
+  // G per stage (srbd_constraints.py:193-222), CCS order over u columns 0..11
+  int g = 0;
+  for (int j = 0; j < 12; ++j) {
+    int rows[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int n = 0;
+    const int f = (j == 3 || j == 4 || j == 5 || j == 10) ? 1 : 0;
+    const int o = 8 * f;
+    if (j == 0 || j == 3) { rows[0] = o + 0; rows[1] = o + 1; n = 2; }
+    if (j == 1 || j == 4) { rows[0] = o + 2; rows[1] = o + 3; n = 2; }
+    if (j == 2 || j == 5) { for (int q = 0; q < 8; ++q) rows[q] = o + q; n = 8; }
+    if (j == 7 || j == 10) { rows[0] = o + 4; rows[1] = o + 5; n = 2; }
+    for (int q = 0; q < n; ++q) {
+      t.gcol[g] = (int8_t)j;
+      t.grow[g] = (int8_t)rows[q];
+      ++g;
+    }
+  }
+  for (int k = 0; k < 16; ++k) t.gr_n[k] = 0;
+  for (int q = 0; q < 28; ++q) {
+    const int k = t.grow[q];
+    t.gr_off[k][t.gr_n[k]] = (int8_t)q;
+    t.gr_col[k][t.gr_n[k]] = t.gcol[q];
+    t.gr_n[k]++;
+  }
+  const int8_t fl[4] = {0, 1, 2, 7}, fr[4] = {3, 4, 5, 10};
+  for (int q = 0; q < 4; ++q) {
+    t.foot_col[0][q] = fl[q];
+    t.foot_col[1][q] = fr[q];
+  }
+  for (int j = 0; j < 12; ++j) {
+    t.col_foot[j] = -1;
+    t.col_pos[j] = -1;
+  }
+  for (int f = 0; f < 2; ++f)
+    for (int q = 0; q < 4; ++q) {
+      t.col_foot[t.foot_col[f][q]] = (int8_t)f;
+      t.col_pos[t.foot_col[f][q]] = (int8_t)q;
+    }
+  return t;
+}
+
+// Pattern tables in constant memory (one translation unit: srbd_mpc.hip).
+static __constant__ Tables c_tab = make_tables();
+
+// Value offsets inside A_val for horizon N.
+__host__ __device__ inline int a_xblock(int k) { return 36 * (k - 1); }  // x_k block, k < N
+__host__ __device__ inline int a_ubase(int N) { return 36 * N - 24; }
+__host__ __device__ inline int a_ublock(int N, int i) { return 36 * N - 24 + 86 * i; }
+__host__ __device__ inline int nnz_A(int N) { return 122 * N - 24; }
+
+// Offset in A_val of the +I entry of x_{i+1}[r] (stage i rows): a full x-column block for
+// i < N-1, the single-entry x_N column for the last stage.
+__host__ __device__ inline int a_pidx(const Tables& t, int N, int i, int r) {
+  return (i < N - 1) ? a_xblock(i + 1) + t.cpx[r] : 36 * (N - 1) + r;
+}
+
+// ------------------------------------------------------------------ wave64 reductions ----
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace srbd

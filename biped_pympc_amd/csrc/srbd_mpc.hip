@@ -1,0 +1,265 @@
+// srbd_mpc.hip -- libsrbd_mpc.so: HIP kernels (gfx950) + the C-ABI of include/srbd_mpc.h.
+//
+// One translation unit so the constant-memory pattern tables (srbd_common.hpp) exist once.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/srbd_mpc.h"
+#include "pdipm.hpp"
+#include "qp_former.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* what) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "%s (code %d: %s)", what, code,
+                code > 0 ? hipGetErrorString((hipError_t)code) : "invalid argument");
+  g_last_error = buf;
+  return code;
+}
+
+constexpr int kFormerWaves = 4;
+constexpr int kErrInvalid = (int)hipErrorInvalidValue;
+
+bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
+
+size_t solver_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::SolverLayout(N).total; }
+
+int ensure_lds_attr(size_t bytes) {
+  static std::mutex mu;
+  static size_t configured = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (bytes <= configured) return 0;
+  hipError_t e = hipFuncSetAttribute((const void*)srbd::pdipm_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return set_error((int)e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  configured = bytes;
+  return 0;
+}
+
+int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
+  if (a.batch == 0) return 0;
+  const int grid = (a.batch + kFormerWaves - 1) / kFormerWaves;
+  hipLaunchKernelGGL(srbd::qp_former_kernel<kFormerWaves>, dim3(grid), dim3(64 * kFormerWaves), 0, s, a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "qp_former_kernel launch");
+}
+
+int launch_solver(const srbd::SolverArgs& a, hipStream_t s) {
+  if (a.batch == 0) return 0;
+  const size_t lds = solver_lds_bytes(a.N);
+  if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
+  if (int rc = ensure_lds_attr(lds)) return rc;
+  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(64), lds, s, a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "pdipm_kernel launch");
+}
+
+// CusADi-style blocking call on the legacy default stream, timed with hipEvents.
+template <class F>
+float timed_blocking(F&& launch) {
+  static std::mutex mu;
+  static hipEvent_t ev0 = nullptr, ev1 = nullptr;  // created once (the reference leaks 2 per call)
+  std::lock_guard<std::mutex> lock(mu);
+  if (!ev0) {
+    if (hipEventCreate(&ev0) != hipSuccess || hipEventCreate(&ev1) != hipSuccess) {
+      set_error((int)hipErrorInitializationError, "hipEventCreate");
+      return -1.0f;
+    }
+  }
+  (void)hipEventRecord(ev0, 0);
+  if (launch() != 0) return -1.0f;
+  (void)hipEventRecord(ev1, 0);
+  hipError_t e = hipEventSynchronize(ev1);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    set_error((int)e, "kernel execution");
+    return -1.0f;
+  }
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, ev0, ev1);
+  return ms / 1000.0f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srbd_abi_version(void) { return SRBD_ABI_VERSION; }
+
+const char* srbd_last_error(void) { return g_last_error.c_str(); }
+
+size_t srbd_solver_lds_bytes(int horizon) { return horizon_ok(horizon) ? solver_lds_bytes(horizon) : 0; }
+
+size_t srbd_mpc_workspace_doubles(int horizon, int batch) {
+  if (!horizon_ok(horizon) || batch < 0) return 0;
+  const size_t N = (size_t)horizon;
+  return (size_t)batch * (24 * N + 24 * N + (122 * N - 24) + 14 * N + 28 * N + 16 * N);
+}
+
+float srbd_evaluate_qp_former(int horizon, const double* inputs[], double* work, double* outputs[],
+                              int batch) {
+  (void)work;
+  if (!horizon_ok(horizon) || batch < 0 || !inputs || !outputs) {
+    set_error(kErrInvalid, "srbd_evaluate_qp_former: bad horizon/batch/pointer table");
+    return -1.0f;
+  }
+  srbd::FormerArgs a{};
+  a.dev_in = inputs;
+  a.dev_out = outputs;
+  a.N = horizon;
+  a.batch = batch;
+  return timed_blocking([&] { return launch_former(a, 0); });
+}
+
+float srbd_evaluate_pdipm(int horizon, int n_iter, const double* inputs[], double* work,
+                          double* outputs[], int batch) {
+  (void)work;
+  if (!horizon_ok(horizon) || n_iter < 1 || batch < 0 || !inputs || !outputs) {
+    set_error(kErrInvalid, "srbd_evaluate_pdipm: bad horizon/n_iter/batch/pointer table");
+    return -1.0f;
+  }
+  srbd::SolverArgs a{};
+  a.dev_in = inputs;
+  a.dev_out = outputs;
+  a.N = horizon;
+  a.n_iter = n_iter;
+  a.batch = batch;
+  a.init_mode = 0;
+  return timed_blocking([&] { return launch_solver(a, 0); });
+}
+
+int srbd_qp_former(int horizon, int batch, const double* const* inputs, double* const* outputs,
+                   void* stream) {
+  if (!horizon_ok(horizon) || batch < 0 || !inputs || !outputs)
+    return set_error(kErrInvalid, "srbd_qp_former: bad arguments");
+  srbd::FormerArgs a{};
+  for (int i = 0; i < 17; ++i) {
+    if (!inputs[i]) return set_error(kErrInvalid, "srbd_qp_former: null input");
+    a.in[i] = inputs[i];
+  }
+  for (int i = 0; i < 6; ++i) {
+    if (!outputs[i]) return set_error(kErrInvalid, "srbd_qp_former: null output");
+    a.out[i] = outputs[i];
+  }
+  a.N = horizon;
+  a.batch = batch;
+  return launch_former(a, (hipStream_t)stream);
+}
+
+static int pdipm_common(int horizon, int n_iter, int batch, double y0, int init_mode,
+                        const double* const* inputs, double* const* outputs, void* stream) {
+  if (!horizon_ok(horizon) || n_iter < 1 || batch < 0 || !inputs || !outputs)
+    return set_error(kErrInvalid, "srbd_pdipm: bad arguments");
+  srbd::SolverArgs a{};
+  const int nin = init_mode ? 6 : 10;
+  for (int i = 0; i < nin; ++i) {
+    if (!inputs[i]) return set_error(kErrInvalid, "srbd_pdipm: null input");
+    a.in[i] = inputs[i];
+  }
+  for (int i = 0; i < 6; ++i) {
+    if (!outputs[i]) return set_error(kErrInvalid, "srbd_pdipm: null output");
+    a.out[i] = outputs[i];
+  }
+  a.N = horizon;
+  a.n_iter = n_iter;
+  a.batch = batch;
+  a.init_mode = init_mode;
+  a.y0 = y0;
+  return launch_solver(a, (hipStream_t)stream);
+}
+
+int srbd_pdipm(int horizon, int n_iter, int batch, const double* const* inputs,
+               double* const* outputs, void* stream) {
+  return pdipm_common(horizon, n_iter, batch, 0.0, 0, inputs, outputs, stream);
+}
+
+int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double* const* inputs,
+                    double* const* outputs, void* stream) {
+  return pdipm_common(horizon, n_iter, batch, y0, 1, inputs, outputs, stream);
+}
+
+int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                   double* qp_workspace, double* const* outputs, void* stream) {
+  if (!horizon_ok(horizon) || !qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve: bad arguments");
+  const size_t N = (size_t)horizon, B = (size_t)(batch < 0 ? 0 : batch);
+  double* H = qp_workspace;
+  double* f = H + B * 24 * N;
+  double* A = f + B * 24 * N;
+  double* b = A + B * (122 * N - 24);
+  double* G = b + B * 14 * N;
+  double* d = G + B * 28 * N;
+  double* qp[6] = {H, f, A, b, G, d};
+  if (int rc = srbd_qp_former(horizon, batch, former_inputs, qp, stream)) return rc;
+  const double* sin[10] = {H, G, A, f, d, b, nullptr, nullptr, nullptr, nullptr};
+  return srbd_pdipm_cold(horizon, n_iter, batch, y0, sin, outputs, stream);
+}
+
+int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind) {
+  if (!horizon_ok(horizon) || !colptr || !rowind) return -1;
+  constexpr srbd::Tables T = srbd::make_tables();
+  const int N = horizon, nz = 24 * N;
+  int nnz = 0;
+  std::vector<int> row, col;
+  auto put = [&](int off, int r, int c) {
+    if (off < 0 || off >= nnz) return false;
+    if (row[off] != -1) return false;  // two entries mapped to one value slot
+    row[off] = r;
+    col[off] = c;
+    return true;
+  };
+  if (which == 0) {
+    nnz = nz;
+    row.assign(nnz, -1);
+    col.assign(nnz, -1);
+    for (int c = 0; c < nz; ++c)
+      if (!put(c, c, c)) return -2;
+  } else if (which == 1) {
+    nnz = srbd::nnz_A(N);
+    row.assign(nnz, -1);
+    col.assign(nnz, -1);
+    for (int i = 0; i < N; ++i) {
+      const int ub = srbd::a_ublock(N, i);
+      for (int r = 0; r < 12; ++r) {
+        if (!put(srbd::a_pidx(T, N, i, r), 12 * i + r, 12 * i + r)) return -2;  // x_{i+1}[r]
+        for (int j = 0; j < 12; ++j) {
+          if (i >= 1 && T.Mi[r][j] >= 0 && !put(srbd::a_xblock(i) + T.Mi[r][j], 12 * i + r, 12 * (i - 1) + j))
+            return -2;
+          if (T.Ni[r][j] >= 0 && !put(ub + T.Ni[r][j], 12 * i + r, 12 * N + 12 * i + j)) return -2;
+        }
+      }
+      if (!put(ub + T.e6, 12 * N + 2 * i, 12 * N + 12 * i + 6)) return -2;
+      if (!put(ub + T.e9, 12 * N + 2 * i + 1, 12 * N + 12 * i + 9)) return -2;
+    }
+  } else if (which == 2) {
+    nnz = 28 * N;
+    row.assign(nnz, -1);
+    col.assign(nnz, -1);
+    for (int i = 0; i < N; ++i)
+      for (int q = 0; q < 28; ++q)
+        if (!put(28 * i + q, 16 * i + T.grow[q], 12 * N + 12 * i + T.gcol[q])) return -2;
+  } else {
+    return -1;
+  }
+  // every slot filled, (col, row) strictly increasing in slot order  => valid sorted CCS
+  for (int k = 0; k < nnz; ++k) {
+    if (row[k] < 0) return -3;
+    if (k > 0 && (col[k] < col[k - 1] || (col[k] == col[k - 1] && row[k] <= row[k - 1]))) return -4;
+  }
+  for (int c = 0; c <= nz; ++c) colptr[c] = 0;
+  for (int k = 0; k < nnz; ++k) {
+    colptr[col[k] + 1]++;
+    rowind[k] = row[k];
+  }
+  for (int c = 0; c < nz; ++c) colptr[c + 1] += colptr[c];
+  return nnz;
+}
+
+}  // extern "C"

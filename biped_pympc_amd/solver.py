@@ -1,0 +1,119 @@
+"""Torch-facing API over libsrbd_mpc.so (extended C-ABI, caller's current HIP stream).
+
+PyTorch supplies device memory and the stream only; all arithmetic runs in the HIP kernels.
+Tensors are batched row-major ``(B, nnz)`` FP64 on the GPU, exactly the CusADi layout
+(reference ``biped_pympc/cusadi/src/CusadiFunction.py:71-76``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from biped_pympc_amd import _native
+from biped_pympc_amd.layout import Dims
+
+
+def _stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check_batch(tensors, widths, B: int, what: str):
+    for i, (t, w) in enumerate(zip(tensors, widths)):
+        if t is None:
+            continue
+        if not t.is_cuda or t.dtype != torch.float64:
+            raise TypeError(f"{what}: input {i} must be a CUDA float64 tensor")
+        if t.numel() != B * w:
+            raise ValueError(f"{what}: input {i} has {t.numel()} elements, expected {B}x{w}")
+        if not t.is_contiguous():
+            raise ValueError(f"{what}: input {i} must be contiguous (CusADi row layout)")
+
+
+def qp_former(inputs: list[torch.Tensor], N: int, outputs: list[torch.Tensor] | None = None):
+    """17 former inputs -> [H, f, A, b, G, d] nonzeros (B, nnz) (srbd_constraints.py:20-81)."""
+    d = Dims(N)
+    B = inputs[0].shape[0]
+    _check_batch(inputs, d.former_in_nnz, B, "qp_former")
+    if outputs is None:
+        outputs = [torch.empty((B, w), dtype=torch.float64, device=inputs[0].device)
+                   for w in d.former_out_nnz]
+    L = _native.lib()
+    rc = L.srbd_qp_former(N, B, _native.ptr_array([t.data_ptr() for t in inputs]),
+                          _native.ptr_array([t.data_ptr() for t in outputs]), _stream_ptr())
+    _native.check(rc, "srbd_qp_former")
+    return outputs
+
+
+def _alloc_solver_outputs(B: int, N: int, device) -> list[torch.Tensor]:
+    return [torch.empty((B, w), dtype=torch.float64, device=device) for w in Dims(N).solver_out_nnz]
+
+
+def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_iter: int,
+          y0: float = 1.0, outputs: list[torch.Tensor] | None = None):
+    """Sparse PDIPM, n_iter Mehrotra iterations (sparse_pdipm_solver.py:357-534).
+
+    qp: [Q_val, G_val, A_val, f, h, b]; iterate: [x, s, z, y] or None for the GPU caller's cold
+    start (x=0, s=max(h,1), z=1, y=y0; mpc_controller_cusadi.py:138-141).
+    Returns [x, s, z, y, residuals(4), mu(1)].
+    """
+    d = Dims(N)
+    B = qp[0].shape[0]
+    ins = list(qp) + (list(iterate) if iterate is not None else [None] * 4)
+    _check_batch(ins, d.solver_in_nnz, B, "pdipm")
+    if outputs is None:
+        outputs = _alloc_solver_outputs(B, N, qp[0].device)
+    L = _native.lib()
+    ptrs = _native.ptr_array([t.data_ptr() if t is not None else 0 for t in ins])
+    outp = _native.ptr_array([t.data_ptr() for t in outputs])
+    if iterate is None:
+        rc = L.srbd_pdipm_cold(N, n_iter, B, float(y0), ptrs, outp, _stream_ptr())
+    else:
+        rc = L.srbd_pdipm(N, n_iter, B, ptrs, outp, _stream_ptr())
+    _native.check(rc, "srbd_pdipm")
+    return outputs
+
+
+@dataclass
+class MPCSolveBuffers:
+    """Preallocated device buffers for repeated ``mpc_solve`` calls (no allocation per step)."""
+    N: int
+    B: int
+    workspace: torch.Tensor
+    outputs: list
+
+    @classmethod
+    def allocate(cls, N: int, B: int, device="cuda") -> "MPCSolveBuffers":
+        n = _native.lib().srbd_mpc_workspace_doubles(N, B)
+        return cls(N, B, torch.empty(max(n, 1), dtype=torch.float64, device=device),
+                   _alloc_solver_outputs(B, N, device))
+
+    def qp_views(self) -> list[torch.Tensor]:
+        """[H, f, A, b, G, d] views into the workspace (filled by the former)."""
+        d = Dims(self.N)
+        out, o = [], 0
+        for w in d.former_out_nnz:
+            out.append(self.workspace[o:o + self.B * w].view(self.B, w))
+            o += self.B * w
+        return out
+
+
+def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float = 1.0,
+              buffers: MPCSolveBuffers | None = None):
+    """qp_former + cold-started PDIPM in one stream with no host synchronisation.
+
+    Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
+    iteration count as a runtime argument. Returns [x, s, z, y, residuals, mu].
+    """
+    d = Dims(N)
+    B = former_inputs[0].shape[0]
+    _check_batch(former_inputs, d.former_in_nnz, B, "mpc_solve")
+    if buffers is None or buffers.B != B or buffers.N != N:
+        buffers = MPCSolveBuffers.allocate(N, B, former_inputs[0].device)
+    L = _native.lib()
+    rc = L.srbd_mpc_solve(N, n_iter, B, float(y0),
+                          _native.ptr_array([t.data_ptr() for t in former_inputs]),
+                          buffers.workspace.data_ptr(),
+                          _native.ptr_array([t.data_ptr() for t in buffers.outputs]), _stream_ptr())
+    _native.check(rc, "srbd_mpc_solve")
+    return buffers.outputs

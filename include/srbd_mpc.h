@@ -1,0 +1,88 @@
+/*
+ * srbd_mpc.h -- C-ABI of the MI355X-native SRBD-MPC QP engine (libsrbd_mpc.so + thin drop-ins).
+ *
+ * Drop-in boundary for the reference's CusADi hot path (rl-augmented-mpc/Biped-PyMPC):
+ *   - `evaluate` below is the exact symbol each CusADi function library exports
+ *     (reference biped_pympc/cusadi/src/generateCUDACode.py:157-183) and that
+ *     CusadiFunction binds through ctypes (biped_pympc/cusadi/src/CusadiFunction.py:28-47).
+ *     Two thin libraries export it: libqp_former.so (CasADi Function 'qp_former',
+ *     srbd_constraints.py:75-79) and libsparse_pdipm_multiple_iterations.so ('sparse_pdipm_multiple_iterations',
+ *     sparse_pdipm_solver.py:532-534), built for the deployed configuration N = 10, 5 iterations
+ *     (mpc_controller_cusadi.py:28; generate_solver_function.py:106). Other horizons/iteration counts
+ *     get libqp_former_N<N>.so / libsparse_pdipm_multiple_iterations_N<N>_K<K>.so.
+ *   - the srbd_* entry points are the extended API (runtime horizon and iteration count, caller's
+ *     HIP stream, fused former+solve), all plain pointers and sizes.
+ *
+ * Memory: every double* is DEVICE memory, batched row-major (batch, nnz) per tensor, exactly the
+ * CusADi layout (input i of env e at inputs[i] + e*nnz_in[i]). The library allocates nothing on
+ * the device; it never calls exit(): failures return an error code and set srbd_last_error().
+ */
+#ifndef SRBD_MPC_H_
+#define SRBD_MPC_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRBD_ABI_VERSION 1
+#define SRBD_MAX_HORIZON 32
+
+/* ---- CusADi ABI (thin per-function libraries) ---------------------------------------------
+ * inputs/outputs: DEVICE pointer to a DEVICE array of n_in / n_out DEVICE pointers
+ * (CusadiFunction.py:84-92). work: ignored (CusADi's (batch, sz_w) scratch; may be NULL).
+ * Blocking, legacy default stream. Returns kernel time in SECONDS (generateCUDACode.py:176-182),
+ * or a negative value on error (the reference's gpuErrchk calls exit(); this never does). */
+float evaluate(const double* inputs[], double* work, double* outputs[], const int batch_size);
+
+/* ---- Extended API (libsrbd_mpc.so) ------------------------------------------------------------ */
+int srbd_abi_version(void);
+const char* srbd_last_error(void);
+
+/* CusADi-ABI implementations with explicit configuration (what the thin libraries call). */
+float srbd_evaluate_qp_former(int horizon, const double* inputs[], double* work, double* outputs[],
+                              int batch);
+float srbd_evaluate_pdipm(int horizon, int n_iter, const double* inputs[], double* work,
+                          double* outputs[], int batch);
+
+/* qp_former: 17 inputs (x0, x, u, x_ref, dt, m, mu, R_body, I_world, body_pos, left_foot_pos,
+ * right_foot_pos, contact_table, Q, R, residual_lin_accel, residual_ang_accel;
+ * srbd_constraints.py:77) -> 6 outputs (nonzeros of H, f, A, b, G, d in CCS order).
+ * `inputs`/`outputs` are HOST arrays of device pointers. Asynchronous on `stream` (hipStream_t,
+ * NULL = default stream). Returns 0 or a hipError_t code. */
+int srbd_qp_former(int horizon, int batch, const double* const* inputs, double* const* outputs,
+                   void* stream);
+
+/* sparse PDIPM: 10 inputs (Q_val, G_val, A_val, f, h, b, x, s, z, y; sparse_pdipm_solver.py:533)
+ * -> 6 outputs (x, s, z, y, residuals[4] = [|rx|, |rs|, |re|, mu_new], mu_new), n_iter >= 1
+ * Newton iterations at run time. Host array of device pointers; asynchronous on `stream`. */
+int srbd_pdipm(int horizon, int n_iter, int batch, const double* const* inputs,
+               double* const* outputs, void* stream);
+
+/* Same, but the iterate is initialised on device as the GPU caller does
+ * (mpc_controller_cusadi.py:138-141): x = 0, s = max(h, 1), z = 1, y = y0. Inputs 6..9 unused
+ * (may be NULL). */
+int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double* const* inputs,
+                    double* const* outputs, void* stream);
+
+/* Whole MPC QP step: qp_former -> cold-start PDIPM (n_iter iterations), one stream, no host sync.
+ * `qp_workspace` is caller-owned device memory of srbd_mpc_workspace_doubles(horizon, batch)
+ * doubles that receives H, f, A, b, G, d (CCS, batched). outputs as srbd_pdipm. */
+size_t srbd_mpc_workspace_doubles(int horizon, int batch);
+int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                   double* qp_workspace, double* const* outputs, void* stream);
+
+/* LDS bytes one solver workgroup (one QP) uses at this horizon (0 if unsupported). */
+size_t srbd_solver_lds_bytes(int horizon);
+
+/* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
+ * offset maps the kernels use to address A_val/G_val. colptr has 24*horizon+1 entries, rowind nnz.
+ * Returns nnz, or a negative value if the kernel's offsets are not a bijection onto a sorted CCS. */
+int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRBD_MPC_H_ */
