@@ -1,0 +1,216 @@
+"""bench.py -- batched SRBD-MPC QP solves/s on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch of synthetic robots per GPU:
+qp_former (HIP) -> cold-started sparse PDIPM (HIP, 10 Mehrotra iterations), i.e. the reference GPU
+caller's QP step (biped_pympc/convex_mpc/mpc_controller_cusadi.py:99-169) at BASELINE config 2
+(batch 4096, horizon N = 10, 10 PDIPM iterations) per GPU; for N > 1 ranks each GPU solves its own
+4096-env shard (weak scaling) and the first-stage inputs u0 (12 doubles/env, the only thing the
+wrapper consumes, mpc_controller_cusadi.py:186) are gathered over RCCL.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (multi-GPU via torch.distributed.run)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from biped_pympc_amd import solver  # noqa: E402
+from biped_pympc_amd.layout import Dims  # noqa: E402
+from biped_pympc_amd.utils.synthetic import make_workload  # noqa: E402
+
+# Structural work per solve, frozen from scripts/algorithmic_work.py (SURVEY.md 8d convention:
+# the reference's sparse LDL^T of its 70N KKT per iteration; bytes = algorithmic HBM traffic).
+WORK = {
+    10: {"flops_per_iter": 75840, "bytes_pdipm_cold": 23688, "bytes_step": 45352,
+         "bytes_former": 3616 + 18048},
+    20: {"flops_per_iter": 165074, "bytes_pdipm_cold": 47528, "bytes_step": 90472,
+         "bytes_former": 6656 + 36288},
+}
+PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD spec; no sparsity)
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch-per-gpu", type=int, default=4096)
+    p.add_argument("--horizon", type=int, default=10)
+    p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--random-gait", action="store_true")
+    p.add_argument("--kernel-reps", type=int, default=10)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def event_time_ms(fn, reps: int) -> float:
+    """Average duration of fn() on torch's current stream (where the kernels are launched)."""
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def load_pmc(N: int, B: int, K: int):
+    """HBM bytes per pdipm launch from the committed rocprofv3 --pmc summary, if one matches."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("horizon") == N and d.get("batch") == B and d.get("iters") == K:
+            return d.get("pdipm_hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    N, K, B = a.horizon, a.iters, a.batch_per_gpu
+    d = Dims(N)
+
+    wl = make_workload(B, N, seed=1000 + rank, random_gait=a.random_gait)
+    inputs = [torch.from_numpy(x).to(dev) for x in wl.inputs]
+    bufs = solver.MPCSolveBuffers.allocate(N, B, dev)
+    u0_all = torch.empty((world * B, 12), dtype=torch.float64, device=dev) if world > 1 else None
+
+    def step():
+        out = solver.mpc_solve(inputs, N, K, y0=1.0, buffers=bufs)
+        if dist is not None:
+            u0 = out[0][:, 12 * N:12 * N + 12].contiguous()
+            dist.all_gather_into_tensor(u0_all, u0)
+        return out
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = 1e3 * elapsed / a.steps
+    value = world * B * a.steps / elapsed
+
+    # per-kernel timing (HIP events on the launch stream), former output already in the workspace
+    qp = bufs.qp_views()
+    sol_qp = [qp[0], qp[4], qp[2], qp[1], qp[5], qp[3]]  # H, G, A, f, h(=d), b
+    pd_out = solver._alloc_solver_outputs(B, N, dev)
+    ms_former = event_time_ms(lambda: solver.qp_former(inputs, N, outputs=qp), a.kernel_reps)
+    ms_pdipm = event_time_ms(lambda: solver.pdipm(sol_qp, None, N, K, 1.0, outputs=pd_out),
+                             a.kernel_reps)
+    ms_gather = None
+    if dist is not None:
+        u0 = bufs.outputs[0][:, 12 * N:12 * N + 12].contiguous()
+        ms_gather = event_time_ms(lambda: dist.all_gather_into_tensor(u0_all, u0), a.kernel_reps)
+
+    w = WORK.get(N)
+    roofline = None
+    if w is not None:
+        flops = w["flops_per_iter"] * K * B
+        achieved = flops / (ms_pdipm * 1e-3) / 1e12
+        traffic, traffic_src = load_pmc(N, B, K)
+        roofline = {
+            "bound": "mfma", "kernel": "pdipm_kernel", "achieved": round(achieved, 4),
+            "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_pdipm, 4),
+            "note": ("FP64 compute roof (vector == matrix peak on MI355X); kernel runs on the "
+                     "FP64 VALU. Flops = the reference's sparse-LDL KKT work per iteration "
+                     "(SURVEY 8d) x iterations x QPs per launch."),
+            "hbm": {"achieved_GBs": round(w["bytes_pdipm_cold"] * B / (ms_pdipm * 1e-3) / 1e9, 2),
+                    "peak_GBs": PEAK_HBM_GBS,
+                    "frac": round(w["bytes_pdipm_cold"] * B / (ms_pdipm * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
+                    "algorithmic_bytes_per_launch": w["bytes_pdipm_cold"] * B},
+        }
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle  # cpu_baseline leg: the oracle as baseline and checker only
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        sample = min(B, 512)
+        sub = [x[:sample] for x in wl.inputs]
+        oracle.mpc_solve(N, K, [x[:8] for x in sub], nthreads=threads)  # symbolic setup + warm
+        solves, t_cpu, ref = 0, 0.0, None
+        while t_cpu < a.cpu_seconds:
+            t1 = time.perf_counter()
+            ref = oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=threads)
+            t_cpu += time.perf_counter() - t1
+            solves += sample
+        cpu = {"value": round(solves / t_cpu, 1), "unit": "solves/s", "cores": threads,
+               "kind": "port",
+               "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs) on the first "
+                          f"{sample} envs of the same workload, {solves // sample} passes, "
+                          f"{t_cpu:.1f} s, N={N}, {K} iterations")}
+        out = step()
+        torch.cuda.synchronize()
+        x = out[0][:sample].cpu().numpy()
+        ug, ur = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
+        du = np.abs(ug - ur)
+        parity = {"max_abs_du": float(du.max()),
+                  "max_rel_du": float((du.max(axis=1) / np.abs(ur).max(axis=1)).max()),
+                  "envs": sample, "vs": "oracle (CPU restatement; CasADi unavailable: parity unpinned)"}
+
+    if rank == 0:
+        line = {
+            "metric": "batched SRBD QP solves/sec (N=10, 10 PDIPM iters)" if (N, K) == (10, 10)
+            else f"batched SRBD QP solves/sec (N={N}, {K} PDIPM iters)",
+            "value": round(value, 1), "unit": "solves/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"SRBD MPC QP step: qp_former + {K}-iteration sparse PDIPM, "
+                                   f"batch {B}/GPU, horizon N={N}"
+                                   + (", randomized gait" if a.random_gait else ", standing gait"),
+                       "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
+                       "pdipm_iters": K, "qp_dims": [d.nz, d.n_eq, d.n_ineq],
+                       "parallelism": f"dp{world}" + (" (u0 all_gather over RCCL)" if world > 1 else "")},
+            "kernels_ms": {"qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
+                           "u0_all_gather": None if ms_gather is None else round(ms_gather, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

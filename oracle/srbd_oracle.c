@@ -455,6 +455,13 @@ int oracle_kkt_stats(int N, int *n, int *nnzK, int *nnzL) {
   return 0;
 }
 
+/* column pointers of L (nnz per column = Lp[j+1] - Lp[j]) for flop accounting */
+int oracle_kkt_lp(int N, int *Lp_out) {
+  if (oracle_prepare_solver(N)) return -1;
+  memcpy(Lp_out, g_pat[N].Lp, sizeof(int) * (g_pat[N].n + 1));
+  return g_pat[N].n;
+}
+
 typedef struct {
   double *Kx, *Lx, *D, *Y;
   int *Li, *Lnz, *Pattern, *Flag;
