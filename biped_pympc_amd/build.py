@@ -52,6 +52,27 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
+def _build_dropin_lib(fn: str, N: int, K: int | None, core: str, force: bool, verbose: bool) -> str:
+    shim = os.path.join(CSRC, "dropin_evaluate.c")
+    out = os.path.join(LIB_DIR, dropin_lib_name(fn, N, K))
+    if not force and _newer(out, [shim, core, os.path.join(INCLUDE, "srbd_mpc.h")]):
+        return out
+    defs = ["-DSRBD_FN_FORMER"] if fn == "qp_former" else ["-DSRBD_FN_PDIPM", f"-DSRBD_ITERS={K}"]
+    cmd = ["gcc", "-O2", "-fPIC", "-shared", f"-DSRBD_N={N}", *defs, "-o", out, shim,
+           f"-L{LIB_DIR}", "-lsrbd_mpc", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    _run(cmd)
+    return out
+
+
+def build_dropin(kind: str, N: int, K: int | None) -> str:
+    """Thin CusADi-ABI library for one (function, horizon, iterations) configuration."""
+    fn = "qp_former" if kind == "qp_former" else "sparse_pdipm_multiple_iterations"
+    core = build()
+    return _build_dropin_lib(fn, N, K, core, False, False)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     core = os.path.join(LIB_DIR, "libsrbd_mpc.so")
@@ -64,17 +85,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-    shim = os.path.join(CSRC, "dropin_evaluate.c")
     for fn, N, K in DROPIN_CONFIGS:
-        out = os.path.join(LIB_DIR, dropin_lib_name(fn, N, K))
-        if not force and _newer(out, [shim, core, os.path.join(INCLUDE, "srbd_mpc.h")]):
-            continue
-        defs = ["-DSRBD_FN_FORMER"] if fn == "qp_former" else ["-DSRBD_FN_PDIPM", f"-DSRBD_ITERS={K}"]
-        cmd = ["gcc", "-O2", "-fPIC", "-shared", f"-DSRBD_N={N}", *defs, "-o", out, shim,
-               f"-L{LIB_DIR}", "-lsrbd_mpc", "-Wl,-rpath,$ORIGIN"]
-        if verbose:
-            print(" ".join(cmd))
-        _run(cmd)
+        _build_dropin_lib(fn, N, K, core, force, verbose)
     return core
 
 

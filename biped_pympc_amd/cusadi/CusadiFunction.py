@@ -1,0 +1,125 @@
+"""Drop-in ``CusadiFunction`` (reference ``biped_pympc/cusadi/src/CusadiFunction.py:6-117``).
+
+Same constructor, attributes and methods -- ``evaluate(inputs)``, ``outputs_sparse[i]``,
+``getDenseOutput(i)``, ``eval_time``, ``checkInputDimensions`` -- bound through ctypes to the same
+``float evaluate(const double**, double*, double**, int)`` symbol of ``lib<fn.name()>.so``, now a
+thin library over the hand-written HIP kernels (``include/srbd_mpc.h``). Differences, all
+deliberate:
+  * ``fn_casadi`` is a ``biped_pympc_amd.cusadi.Function`` descriptor (no CasADi dependency);
+  * a failing kernel raises ``RuntimeError`` with the library's message instead of the reference's
+    ``exit(code)`` inside ``gpuErrchk`` (``generateCUDACode.py:106-112``);
+  * the device pointer tables are refreshed with one host->device copy instead of one per element,
+    and ``getDenseOutput`` caches its scatter indices (same results).
+As in the reference, the caller's tensors are used in place through ``data_ptr()`` and their
+strides are NOT consulted: pass contiguous ``(num_instances, nnz_in[i])`` FP64 CUDA tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import torch
+
+from biped_pympc_amd.build import LIB_DIR, build_dropin
+
+
+class CusadiFunction:
+    # Public variables:
+    fn_casadi = None
+    fn_name = None
+    num_instances = 0
+    inputs_sparse = []
+    outputs_sparse = []
+    outputs_dense = []
+
+    # Private variables:
+    _device = "cuda"
+
+    def __init__(self, fn_casadi, num_instances: int):
+        assert torch.cuda.is_available()
+        lib_filepath = os.path.join(LIB_DIR, f"lib{fn_casadi.name()}.so")
+        if not os.path.exists(lib_filepath):
+            build_dropin(fn_casadi.kind, fn_casadi.horizon, fn_casadi.n_iter)
+        self.fn_casadi = fn_casadi
+        self.fn_name = fn_casadi.name()
+        self.num_instances = int(num_instances)
+        self._fn_library = ctypes.CDLL(lib_filepath)
+        self._fn_library.evaluate.restype = ctypes.c_float
+        self._fn_library.evaluate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int]
+        self._core = ctypes.CDLL(os.path.join(LIB_DIR, "libsrbd_mpc.so"))
+        self._core.srbd_last_error.restype = ctypes.c_char_p
+        self._dense_index = {}
+        self.eval_time = 0.0
+        print("Loaded CasADi function: ", self.fn_casadi)
+        print("Loaded library: ", self._fn_library)
+        self._setup()
+
+    def evaluate(self, inputs):
+        self._clearTensors()
+        self._prepareInputTensor(inputs)
+        t = self._fn_library.evaluate(self._fn_input, self._fn_work, self._fn_output,
+                                      self.num_instances)
+        if t < 0:
+            raise RuntimeError(f"{self.fn_name}: {self._core.srbd_last_error().decode(errors='replace')}")
+        self.eval_time = t
+
+    def getDenseOutput(self, out_idx=None):
+        fn = self.fn_casadi
+        if out_idx not in self._dense_index:
+            rows, cols = fn.sparsity_out(out_idx).get_triplet()
+            lin = torch.tensor(rows, dtype=torch.int64) * fn.size2_out(out_idx) + torch.tensor(cols, dtype=torch.int64)
+            self._dense_index[out_idx] = lin.to(self._device)
+        lin = self._dense_index[out_idx]
+        s1, s2 = fn.size1_out(out_idx), fn.size2_out(out_idx)
+        dense = torch.zeros((self.num_instances, s1 * s2), device=self._device, dtype=torch.double)
+        dense.index_put_((slice(None), lin), self.outputs_sparse[out_idx].reshape(self.num_instances, -1),
+                         accumulate=True)
+        return dense.view(self.num_instances, s1, s2)
+
+    def checkInputDimensions(self, inputs):
+        """Shape check of every input (the reference runs one CPU CasADi call, :60-67)."""
+        fn = self.fn_casadi
+        ok = len(inputs) == fn.n_in() and all(
+            t.numel() == self.num_instances * fn.nnz_in(i) and t.dtype == torch.double
+            for i, t in enumerate(inputs))
+        if ok:
+            print("Input check successful. Tensor dimensions are correct for inputs.")
+        else:
+            print("Error in input dimensions. Exiting...")
+            sys.exit(1)
+
+    # ! Private methods:
+    def _setup(self):
+        fn = self.fn_casadi
+        B = self.num_instances
+        self._input_tensors = [torch.zeros((B, fn.nnz_in(i)), device=self._device, dtype=torch.double)
+                               for i in range(fn.n_in())]
+        self._output_tensors = [torch.zeros(B, fn.nnz_out(i), device=self._device, dtype=torch.double)
+                                for i in range(fn.n_out())]
+        self._output_tensors_dense = [torch.zeros((B, fn.size1_out(i), fn.size2_out(i)),
+                                                  device=self._device, dtype=torch.double)
+                                      for i in range(fn.n_out())]
+        self._work_tensor = torch.zeros((B, max(fn.sz_w(), 1)), device=self._device, dtype=torch.double)
+        self._input_ptrs = torch.zeros(fn.n_in(), device=self._device, dtype=torch.int64)
+        self._output_ptrs = torch.tensor([t.data_ptr() for t in self._output_tensors],
+                                         device=self._device, dtype=torch.int64)
+        self._fn_input = ctypes.c_void_p(self._input_ptrs.data_ptr())
+        self._fn_output = ctypes.c_void_p(self._output_ptrs.data_ptr())
+        self._fn_work = ctypes.c_void_p(self._work_tensor.data_ptr())
+        self.inputs_sparse = self._input_tensors
+        self.outputs_sparse = self._output_tensors
+        self.outputs_dense = self._output_tensors_dense
+
+    def _prepareInputTensor(self, inputs):
+        for i in range(self.fn_casadi.n_in()):
+            self._input_tensors[i] = inputs[i]
+        self._input_ptrs.copy_(torch.tensor([t.data_ptr() for t in self._input_tensors],
+                                            dtype=torch.int64))
+        self.inputs_sparse = self._input_tensors
+
+    def _clearTensors(self):
+        for t in self._output_tensors:
+            t.zero_()
+        self._work_tensor.zero_()

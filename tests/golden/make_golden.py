@@ -1,0 +1,107 @@
+"""Generate the committed golden fixtures (run from the repo root; CPU only).
+
+srbd_oracle_N{10,20}.npz -- named inputs and the oracle's qp_former + PDIPM outputs.
+    Regression pins for the oracle and the parity targets for the GPU tests. Inputs:
+      env 0: demo point of srbd_constraints.py:244-282 (dt 0.04, m 13.5, mu 0.5, R = I, ...)
+      env 1: demo point of generate_solver_function.py:19-58 (its Q/R weights)
+      env 2-3: SURVEY 8d synthetic robots (standing gait), env 4-5: randomized gait + residuals.
+    The reference itself cannot produce these (CasADi absent): parity unpinned.
+gait_reference.npz -- contact tables from the REFERENCE GaitGenerator.mpc_gait, imported
+    standalone from /root/reference (gait_generator.py needs only torch), for the device-side
+    contact-schedule row. Skipped when /root/reference is absent.
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from biped_pympc_amd.layout import Dims  # noqa: E402
+from biped_pympc_amd.utils.synthetic import make_workload, solver_init  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+ITERS = (1, 5, 10, 20)
+
+
+def demo_inputs(N, variant):
+    """Single-env former inputs at the reference's demo points."""
+    m = 13.5
+    body = np.array([0.0, 0.0, 0.5])
+    lf, rf = np.array([0.1, 0.05, 0.0]), np.array([0.1, -0.05, 0.0])
+    z = np.zeros(24 * N)
+    for i in range(N):
+        z[i * 12 + 5] = 0.5
+        u = 12 * N + 12 * i
+        z[u + 2] = m * 9.81 / 2
+        z[u + 5] = m * 9.81 / 2
+        z[u + 6:u + 9] = np.cross(lf - body, z[u:u + 3])
+        z[u + 9:u + 12] = np.cross(rf - body, z[u + 3:u + 6])
+    xref = np.zeros(12 * N)
+    xref[5::12] = 0.55
+    x0 = np.zeros(12)
+    x0[5] = 0.55
+    if variant == 0:  # srbd_constraints.py:244-282
+        dt, mu = 0.04, 0.5
+        Q = np.array([50, 50, 10, 10, 10, 100, 10, 10, 10, 10, 10, 10], float)
+        R = np.full(12, 1e-1)
+    else:  # generate_solver_function.py:19-58
+        dt, mu = 0.04, 0.5
+        Q = np.array([200, 500, 500, 500, 500, 500, 1, 1, 5, 1, 1, 5], float)
+        R = np.array([1e-5] * 6 + [1e-2] * 6)
+    Iw = np.diag([0.5413, 0.52, 0.0691])
+    return [x0, z[:12 * N], z[12 * N:], xref, np.array([dt]), np.array([m]), np.array([mu]),
+            np.eye(3).reshape(-1), Iw.reshape(-1), body, lf, rf, np.ones(2 * N), Q, R,
+            np.zeros(3), np.zeros(3)]
+
+
+def former_fixture(N):
+    d = Dims(N)
+    envs = [demo_inputs(N, 0), demo_inputs(N, 1)]
+    a = make_workload(2, N, seed=2024)
+    b = make_workload(2, N, seed=2025, random_gait=True, residuals=True)
+    inputs = []
+    for k, w in enumerate(d.former_in_nnz):
+        rows = [np.asarray(e[k], float).reshape(w) for e in envs]
+        rows += [a.inputs[k][j] for j in range(2)] + [b.inputs[k][j] for j in range(2)]
+        inputs.append(np.stack(rows))
+    return inputs
+
+
+def main():
+    for N in (10, 20):
+        inputs = former_fixture(N)
+        H, f, A, b, G, d = oracle.qp_former(N, inputs)
+        data = {f"in{k}": v for k, v in enumerate(inputs)}
+        data.update(H=H, f=f, A=A, b=b, G=G, d=d)
+        x, s, z, y = solver_init(d, N, y0=1.0)
+        for K in ITERS:
+            out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, z, y])
+            for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
+                data[f"K{K}_{name}"] = v
+        np.savez_compressed(os.path.join(OUT, f"srbd_oracle_N{N}.npz"), **data)
+        print("wrote", f"srbd_oracle_N{N}.npz")
+    gg = "/root/reference/biped_pympc/core/gait/gait_generator.py"
+    if os.path.exists(gg):
+        import torch
+        spec = importlib.util.spec_from_file_location("ref_gait_generator", gg)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        rng = np.random.default_rng(7)
+        B, H = 64, 10
+        ssp = rng.integers(3, 7, (B, 2))
+        dsp = rng.integers(0, 3, (B, 2))
+        phase = rng.uniform(0, 1, B).astype(np.float32)
+        gen = mod.GaitGenerator(B, H, 0.001, torch.full((B,), 0.025), torch.tensor(dsp),
+                                torch.tensor(ssp))
+        gen.gait_phase = torch.tensor(phase)
+        table = gen.mpc_gait.numpy().copy()
+        np.savez_compressed(os.path.join(OUT, "gait_reference.npz"), ssp=ssp, dsp=dsp,
+                            phase=phase, table=table)
+        print("wrote gait_reference.npz")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""The C-ABI boundary without a GPU: libraries load, export exactly what include/*.h declares,
+and reject bad arguments with an error code + message (never exit(), unlike the reference's
+gpuErrchk, generateCUDACode.py:106-112). No compute call is made here."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from biped_pympc_amd import _native, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", src, flags=re.M):
+            if m.group(1) not in ("if", "defined"):
+                names.add(m.group(1))
+    return names
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True)
+    return {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+
+
+def test_header_declares_the_cusadi_symbol_and_extended_api():
+    names = _declared_functions()
+    assert "evaluate" in names
+    assert {"srbd_qp_former", "srbd_pdipm", "srbd_pdipm_cold", "srbd_mpc_solve",
+            "srbd_last_error", "srbd_abi_version"} <= names
+
+
+def test_core_library_exports_every_declared_symbol():
+    build.build()
+    exports = _exports(_native.lib_path())
+    missing = (_declared_functions() - {"evaluate"}) - exports
+    assert not missing, missing
+
+
+@pytest.mark.parametrize("fn,N,K", build.DROPIN_CONFIGS)
+def test_dropin_libraries_export_evaluate(fn, N, K):
+    path = os.path.join(build.LIB_DIR, build.dropin_lib_name(fn, N, K))
+    assert os.path.exists(path)
+    assert "evaluate" in _exports(path)
+    lib = ctypes.CDLL(path)  # resolves libsrbd_mpc.so through rpath $ORIGIN
+    assert lib.evaluate
+
+
+def test_reference_library_names():
+    # CusadiFunction loads lib{fn.name()}.so (CusadiFunction.py:30; setup.sh:10-11)
+    assert build.dropin_lib_name("qp_former", 10, None) == "libqp_former.so"
+    assert build.dropin_lib_name("sparse_pdipm_multiple_iterations", 10, 5) == \
+        "libsparse_pdipm_multiple_iterations.so"
+
+
+def test_abi_introspection():
+    L = _native.lib()
+    assert L.srbd_abi_version() == 1
+    for N in (1, 10, 20, 32):
+        lds = L.srbd_solver_lds_bytes(N)
+        assert 0 < lds <= 160 * 1024
+    assert L.srbd_solver_lds_bytes(0) == 0 and L.srbd_solver_lds_bytes(33) == 0
+    assert L.srbd_mpc_workspace_doubles(10, 4096) == 4096 * 2256
+
+
+def test_bad_arguments_return_errors_without_touching_the_gpu():
+    L = _native.lib()
+    nulls = _native.ptr_array([0] * 17)
+    assert L.srbd_qp_former(0, 4, nulls, nulls, None) != 0
+    assert "bad arguments" in _native.last_error()
+    assert L.srbd_pdipm(10, 0, 4, nulls, nulls, None) != 0  # n_iter must be >= 1
+    assert L.srbd_pdipm(10, 5, 4, nulls, nulls, None) != 0  # null pointers
+    assert "null input" in _native.last_error()
+    assert L.srbd_evaluate_pdipm(40, 5, None, None, None, 4) < 0

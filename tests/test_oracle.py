@@ -1,0 +1,156 @@
+"""Pin the CPU oracle (no GPU): golden regression, an independent dense restatement, closed-form
+model algebra, and the QP's own optimality conditions.
+
+CasADi is unavailable, so nothing here can compare against the reference's own evaluation
+(parity unpinned); these are the strongest available pins.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from biped_pympc_amd import layout
+from biped_pympc_amd.utils.synthetic import make_workload, mpc_gait_table, solver_init
+from oracle import oracle
+from oracle.pdipm_dense import pdipm_dense
+from tests._util import rel_err, rel_err_rows
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _golden(N):
+    z = np.load(os.path.join(GOLDEN, f"srbd_oracle_N{N}.npz"))
+    inputs = [z[f"in{k}"] for k in range(17)]
+    return z, inputs
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_oracle_reproduces_golden(N):
+    z, inputs = _golden(N)
+    H, f, A, b, G, d = oracle.qp_former(N, inputs)
+    for name, v in zip("HfAbGd", (H, f, A, b, G, d)):
+        assert np.array_equal(v, z[name]), name
+    x, s, zz, y = solver_init(d, N)
+    for K in (1, 5, 10, 20):
+        out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, zz, y])
+        for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
+            assert rel_err(v, z[f"K{K}_{name}"]) < 1e-13, (K, name)
+
+
+@pytest.mark.parametrize("K", [1, 3, 5, 10])
+def test_sparse_ldl_oracle_matches_dense_lu_restatement(K):
+    """Two independent restatements of sparse_pdipm_multiple_iterations (sparse LDL^T under a
+    minimum-degree ordering vs dense LU with pivoting) agree to round-off."""
+    N = 10
+    z, inputs = _golden(N)
+    H, f, A, b, G, d = (z[k] for k in "HfAbGd")
+    x, s, zz, y = solver_init(d, N)
+    out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, zz, y])
+    for e in range(H.shape[0]):
+        ref = pdipm_dense(N, K, H[e], G[e], A[e], f[e], d[e], b[e], x[e], s[e], zz[e], y[e])
+        for k in range(4):
+            assert rel_err(out[k][e], ref[k]) < 1e-8, (e, k)
+
+
+def test_pdipm_converges_to_kkt_point():
+    """After many iterations the iterate satisfies the QP's KKT conditions (independent of how the
+    Newton systems are factorised): stationarity, primal feasibility, complementarity."""
+    N = 10
+    z, inputs = _golden(N)
+    H, f, A, b, G, d = (z[k] for k in "HfAbGd")
+    x, s, zz, y = solver_init(d, N)
+    xo, so, zo, yo, res, mu = oracle.pdipm(N, 60, [H, G, A, f, d, b, x, s, zz, y])
+    Hd = layout.to_dense(H, *layout.ccs_H(N), (240, 240))
+    Ad = layout.to_dense(A, *layout.ccs_A(N), (140, 240))
+    Gd = layout.to_dense(G, *layout.ccs_G(N), (160, 240))
+    for e in range(H.shape[0]):
+        stat = Hd[e] @ xo[e] + f[e] + Gd[e].T @ zo[e] + Ad[e].T @ yo[e]
+        scale = 1.0 + np.abs(f[e]).max()
+        assert np.abs(stat).max() < 1e-5 * scale
+        assert np.abs(Ad[e] @ xo[e] - b[e]).max() < 1e-8
+        assert (Gd[e] @ xo[e] - d[e]).max() < 1e-6
+        assert (so[e] * zo[e]).max() < 1e-4
+        assert zo[e].min() >= 1e-8 and so[e].min() >= 1e-8
+
+
+def _closed_form_model(inp):
+    """Numpy closed form of the discrete model, SURVEY.md A.1 (independent of the oracle's AD)."""
+    dt, m = inp[4][0], inp[5][0]
+    R = inp[7].reshape(3, 3, order="F")
+    Iw = inp[8].reshape(3, 3, order="F")
+    Ii = np.linalg.inv(Iw)
+    pb, pl, pr = inp[9], inp[10], inp[11]
+
+    def skew(v):
+        return np.array([[0, -v[2], v[1]], [v[2], 0, -v[0]], [-v[1], v[0], 0]])
+
+    Ac = np.zeros((12, 12))
+    Ac[0:3, 6:9] = R
+    Ac[3:6, 9:12] = np.eye(3)
+    Bc = np.zeros((12, 12))
+    Bc[6:9, 0:3] = Ii @ skew(pl - pb)
+    Bc[6:9, 3:6] = Ii @ skew(pr - pb)
+    Bc[6:9, 6:9] = Ii
+    Bc[6:9, 9:12] = Ii
+    Bc[9:12, 0:3] = np.eye(3) / m
+    Bc[9:12, 3:6] = np.eye(3) / m
+    cc = np.zeros(12)
+    cc[6:9] = inp[16]
+    cc[9:12] = np.array([0, 0, -9.81]) + inp[15]
+    T = dt * np.eye(12) + 0.5 * dt * dt * Ac
+    return np.eye(12) + dt * Ac, T @ Bc, T @ cc
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_former_matches_closed_form_rk4(N):
+    """The oracle's AD Jacobian of the literal RK4 equals the affine closed form
+    A_d = I + dt Ac, B_d = (dt I + dt^2/2 Ac) Bc (Ac^2 = 0), and b = [A_d x0 + c_d; c_d; 0]."""
+    z, inputs = _golden(N)
+    A = layout.to_dense(z["A"], *layout.ccs_A(N), (14 * N, 24 * N))
+    for e in range(A.shape[0]):
+        inp = [v[e] for v in inputs]
+        Ad, Bd, cd = _closed_form_model(inp)
+        for i in range(N):
+            blk = A[e, 12 * i:12 * i + 12]
+            assert np.allclose(blk[:, 12 * N + 12 * i:12 * N + 12 * i + 12], -Bd, rtol=0, atol=1e-14)
+            assert np.allclose(blk[:, 12 * i:12 * i + 12], np.eye(12), atol=0)
+            if i >= 1:
+                assert np.allclose(blk[:, 12 * (i - 1):12 * i], -Ad, rtol=0, atol=1e-15)
+        bexp = np.concatenate([Ad @ inp[0] + cd] + [cd] * (N - 1) + [np.zeros(2 * N)])
+        assert np.allclose(z["b"][e], bexp, rtol=1e-12, atol=1e-13)
+        # H = diag(Q.., R..), f = -Q x_ref (x part), 0 (u part), d = F_max * contact on rows 7, 15
+        assert np.array_equal(z["H"][e], np.concatenate([np.tile(inp[13], N), np.tile(inp[14], N)]))
+        assert np.allclose(z["f"][e][:12 * N], -np.tile(inp[13], N) * inp[3], rtol=1e-12, atol=1e-12)
+        assert np.all(z["f"][e][12 * N:] == 0)
+        ct = inp[12].reshape(N, 2, order="F")
+        dexp = np.zeros(16 * N)
+        dexp[7::16] = 500.0 * ct[:, 0]
+        dexp[15::16] = 500.0 * ct[:, 1]
+        assert np.allclose(z["d"][e], dexp, atol=1e-12)
+
+
+def test_former_pattern_covers_every_nonzero():
+    """oracle.qp_former raises if its dense AD Jacobian has a nonzero outside the CCS pattern."""
+    for seed, gait in ((0, False), (1, True)):
+        wl = make_workload(16, 10, seed=seed, random_gait=gait, residuals=gait)
+        oracle.qp_former(10, wl.inputs)
+
+
+def test_gait_restatement_matches_reference_generator():
+    """utils.synthetic.mpc_gait_table vs the reference GaitGenerator.mpc_gait (fixture generated by
+    importing /root/reference/.../gait_generator.py; tests/golden/make_golden.py)."""
+    g = np.load(os.path.join(GOLDEN, "gait_reference.npz"))
+    tab = mpc_gait_table(g["phase"], g["ssp"], g["dsp"], g["table"].shape[1])
+    assert np.array_equal(tab, g["table"])
+
+
+def test_kkt_symbolic_stats():
+    # structural numbers quoted in SURVEY.md 8(a) a7.1 and frozen in bench.py
+    st10, st20 = oracle.kkt_stats(10), oracle.kkt_stats(20)
+    assert (st10["n"], st10["nnz_kkt"], st10["nnz_L"]) == (700, 3972, 3142)
+    assert (st20["n"], st20["nnz_kkt"], st20["nnz_L"]) == (1400, 7992, 6689)
+
+
+def test_rel_err_rows_helper():
+    a = np.array([[1.0, 2.0], [3.0, 4.0]])
+    assert np.all(rel_err_rows(a, a) == 0)
