@@ -57,6 +57,8 @@ def lib() -> ctypes.CDLL:
     L.srbd_evaluate_pdipm.restype = ctypes.c_float
     L.srbd_evaluate_pdipm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int]
+    L.srbd_set_solver_path.restype = ctypes.c_int
+    L.srbd_set_solver_path.argtypes = [ctypes.c_int]
     L.srbd_pattern_ccs.restype = ctypes.c_int
     L.srbd_pattern_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_int)]
@@ -73,6 +75,21 @@ def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().srbd_last_error().decode(errors="replace")
         raise RuntimeError(f"{what} failed: {msg}")
+
+
+class solver_path:
+    """Context manager selecting the solver kernels: "auto" (fast stage-invariant kernel +
+    general fallback) or "general" (general kernel only). Process-wide; for tests/benchmarks."""
+
+    def __init__(self, path: str):
+        self.code = {"auto": 0, "general": 1}[path]
+
+    def __enter__(self):
+        check(lib().srbd_set_solver_path(self.code), "srbd_set_solver_path")
+        return self
+
+    def __exit__(self, *exc):
+        lib().srbd_set_solver_path(0)
 
 
 def last_error() -> str:

@@ -38,8 +38,11 @@ struct SolverArgs {
   int n_iter;
   int batch;
   int init_mode;  // 0: iterate from inputs 6..9; 1: x=0, s=max(h,1), z=1, y=y0 (GPU caller init)
+  int only_flagged;  // 1: solve only QPs the fast kernel flagged (mu output == kFallbackBits)
   double y0;
 };
+
+constexpr unsigned long long kFallbackBits = 0x7FF8DEADBEEF5A5Aull;  // quiet NaN with a payload
 
 __device__ inline const double* solver_in(const SolverArgs& a, int i) {
   return a.dev_in ? a.dev_in[i] : a.in[i];
@@ -508,6 +511,9 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = blockIdx.x;
   if (env >= args.batch) return;
+  if (args.only_flagged &&
+      __double_as_longlong(solver_out(args, 5)[env]) != (long long)kFallbackBits)
+    return;
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;

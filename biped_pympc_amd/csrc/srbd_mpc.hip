@@ -11,6 +11,7 @@
 
 #include "../../include/srbd_mpc.h"
 #include "pdipm.hpp"
+#include "pdipm_srbd.hpp"
 #include "qp_former.hpp"
 
 namespace {
@@ -31,16 +32,18 @@ constexpr int kErrInvalid = (int)hipErrorInvalidValue;
 bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 
 size_t solver_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::SolverLayout(N).total; }
+size_t fast_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::FastLayout(N).total; }
 
-int ensure_lds_attr(size_t bytes) {
+// 0 = auto (fast stage-invariant kernel, general kernel for flagged QPs); 1 = general kernel only
+int g_solver_path = 0;
+
+int ensure_lds_attr(const void* fn, size_t bytes, size_t* configured) {
   static std::mutex mu;
-  static size_t configured = 0;
   std::lock_guard<std::mutex> lock(mu);
-  if (bytes <= configured) return 0;
-  hipError_t e = hipFuncSetAttribute((const void*)srbd::pdipm_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (bytes <= *configured) return 0;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   if (e != hipSuccess) return set_error((int)e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
-  configured = bytes;
+  *configured = bytes;
   return 0;
 }
 
@@ -52,11 +55,23 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
   return e == hipSuccess ? 0 : set_error((int)e, "qp_former_kernel launch");
 }
 
-int launch_solver(const srbd::SolverArgs& a, hipStream_t s) {
-  if (a.batch == 0) return 0;
+int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
+  if (a0.batch == 0) return 0;
+  static size_t cfg_general = 0, cfg_fast = 0;
+  srbd::SolverArgs a = a0;
+  a.only_flagged = 0;
+  if (g_solver_path == 0) {
+    const size_t lds = fast_lds_bytes(a.N);
+    if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
+    if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_kernel, lds, &cfg_fast)) return rc;
+    hipLaunchKernelGGL(srbd::pdipm_srbd_kernel, dim3(a.batch), dim3(64), lds, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_kernel launch");
+    a.only_flagged = 1;  // general kernel picks up the QPs that are not stage-invariant
+  }
   const size_t lds = solver_lds_bytes(a.N);
   if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
-  if (int rc = ensure_lds_attr(lds)) return rc;
+  if (int rc = ensure_lds_attr((const void*)srbd::pdipm_kernel, lds, &cfg_general)) return rc;
   hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(64), lds, s, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "pdipm_kernel launch");
@@ -97,6 +112,12 @@ int srbd_abi_version(void) { return SRBD_ABI_VERSION; }
 const char* srbd_last_error(void) { return g_last_error.c_str(); }
 
 size_t srbd_solver_lds_bytes(int horizon) { return horizon_ok(horizon) ? solver_lds_bytes(horizon) : 0; }
+
+int srbd_set_solver_path(int path) {
+  if (path != 0 && path != 1) return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto) or 1 (general)");
+  g_solver_path = path;
+  return 0;
+}
 
 size_t srbd_mpc_workspace_doubles(int horizon, int batch) {
   if (!horizon_ok(horizon) || batch < 0) return 0;

@@ -76,6 +76,11 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 /* LDS bytes one solver workgroup (one QP) uses at this horizon (0 if unsupported). */
 size_t srbd_solver_lds_bytes(int horizon);
 
+/* Solver kernel selection: 0 = auto (default): the fast kernel for stage-invariant QPs (every QP
+ * qp_former emits), the general kernel for any other QP in the batch; 1 = general kernel only.
+ * Results agree to round-off (tests/test_gpu_parity.py). Process-wide. */
+int srbd_set_solver_path(int path);
+
 /* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
  * offset maps the kernels use to address A_val/G_val. colptr has 24*horizon+1 entries, rowind nnz.
  * Returns nnz, or a negative value if the kernel's offsets are not a bijection onto a sorted CCS. */

@@ -107,3 +107,71 @@ def test_iteration_schedule_composes():
     torch.cuda.synchronize()
     for a, c in zip(one[:4], cur):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("N,K", [(10, 10), (20, 10), (10, 20)])
+def test_fast_and_general_kernels_agree(N, K):
+    """The stage-invariant fast kernel and the general kernel solve the same systems."""
+    from biped_pympc_amd import _native
+    B = 128
+    wl = make_workload(B, N, seed=31 + K, random_gait=True)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    qp = _cuda([H, G, A, f, d, b])
+    it = _cuda(list(solver_init(d, N)))
+    fast = solver.pdipm(qp, it, N, K)
+    with _native.solver_path("general"):
+        gen = solver.pdipm(qp, it, N, K)
+    torch.cuda.synchronize()
+    tol = 1e-7 if K <= 10 else 1e-4
+    for k in range(4):
+        e = rel_err_rows(fast[k].cpu().numpy(), gen[k].cpu().numpy())
+        assert e.max() <= tol, (k, e.max())
+
+
+def test_mixed_batch_routes_non_invariant_qps_to_the_general_kernel():
+    N, K, B = 10, 10, 96
+    wl = make_workload(B, N, seed=77)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    A = A.copy()
+    G = G.copy()
+    A[::3, 36 * 4 + 7] *= 1.0 + 1e-3   # perturb one stage's -A_d entry in every third QP
+    G[1::3, 28 * 5 + 6] *= 0.9          # and one stage's G entry in others
+    x, s, z, y = solver_init(d, N)
+    ins = [H, G, A, f, d, b, x, s, z, y]
+    ref = oracle.pdipm(N, K, ins)
+    out = solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K)
+    torch.cuda.synchronize()
+    for k in range(4):
+        e = rel_err_rows(out[k].cpu().numpy(), ref[k])
+        assert np.all(np.isfinite(out[k].cpu().numpy()))
+        assert e.max() <= 1e-6, (k, e.max())
+    assert np.all(np.isfinite(out[5].cpu().numpy()))  # no fallback sentinel left behind
+
+
+@pytest.mark.parametrize("fn_kind", ["qp_former", "pdipm"])
+def test_cusadi_dropin_random_inputs(fn_kind):
+    """run_cusadi_function_test.py's harness: random (B, nnz_in) FP64 inputs through the drop-in
+    CusadiFunction (ctypes -> lib<name>.so evaluate) vs per-env CPU evaluation (the oracle)."""
+    from biped_pympc_amd.cusadi import CusadiFunction, pdipm_function, qp_former_function
+    N, B = 10, 256
+    fn = qp_former_function(N) if fn_kind == "qp_former" else pdipm_function(N, 5)
+    g = torch.Generator().manual_seed(0)
+    inputs = [torch.rand((B, fn.nnz_in(i)), generator=g, dtype=torch.float64) for i in range(fn.n_in())]
+    if fn_kind == "qp_former":
+        # keep the 3x3 inertia invertible and the mass/dt positive, as any physical input is
+        inputs[8] = (torch.eye(3, dtype=torch.float64).reshape(1, 9) * 0.5 + 0.1 * inputs[8])
+    else:
+        inputs[7] += 0.1  # slacks and duals strictly positive (interior point)
+        inputs[8] += 0.1
+    cf = CusadiFunction(fn, B)
+    cf.evaluate([t.cuda().contiguous() for t in inputs])
+    torch.cuda.synchronize()
+    assert cf.eval_time > 0
+    np_in = [t.numpy() for t in inputs]
+    ref = oracle.qp_former(N, np_in) if fn_kind == "qp_former" else oracle.pdipm(N, 5, np_in)
+    for k in range(fn.n_out()):
+        err = rel_err_rows(cf.outputs_sparse[k].cpu().numpy(), ref[k])
+        assert err.max() <= (1e-12 if fn_kind == "qp_former" else 1e-6), (k, err.max())
+    dense = cf.getDenseOutput(2 if fn_kind == "qp_former" else 0).cpu().numpy()
+    if fn_kind == "qp_former":
+        assert np.allclose(dense, layout.to_dense(ref[2], *layout.ccs_A(N), (14 * N, 24 * N)), atol=1e-12)
