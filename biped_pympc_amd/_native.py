@@ -21,7 +21,8 @@ class NativeLibraryMissing(RuntimeError):
 
 
 def lib_path() -> str:
-    return os.path.join(LIB_DIR, _LIB_NAME)
+    # SRBD_LIB may point at a diagnostic build (scripts/phase_profile.py); default: the product lib
+    return os.environ.get("SRBD_LIB") or os.path.join(LIB_DIR, _LIB_NAME)
 
 
 def lib() -> ctypes.CDLL:

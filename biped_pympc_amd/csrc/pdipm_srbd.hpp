@@ -23,7 +23,7 @@ namespace srbd {
 
 
 struct FastLayout {
-  int Md, Nd, Cd, Gd, K0, K1, Pd, IX, Hu, SG, PH, DV, X, S, Z, Y, RX, RS, RE, WD, DI, VV, R1T, TV, QV, WV,
+  int Md, Nd, Cd, Gd, K0, K1, Pd, IX, Hu, SG, PH, DV, X, S, Z, Y, RX, RS, RE, WD, DI, VV, TV, QV, WV,
       DS, DZ, DY, SC, total;
   __host__ __device__ FastLayout(int N) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
@@ -35,12 +35,64 @@ struct FastLayout {
     X = take(nz); S = take(m); Z = take(m); Y = take(p);
     RX = take(nz); RS = take(m); RE = take(p);
     WD = take(m); DI = take(m); VV = take(m);
-    R1T = take(nz); TV = take(nz); QV = take(nd); WV = take(nd);
+    TV = take(nz); QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
-    SC = take(160);
+    SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector
     total = o;
   }
 };
+
+// lane k of every 16-lane DPP row -> the whole row (k compile-time after unrolling); one
+// v_mov_b64_dpp row_newbcast (gfx90a+ 64-bit DPP) per broadcast
+#define SRBD_BC16_CASE(K) \
+  case K:                 \
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xF, 0xF, true);
+__device__ __forceinline__ double bc16(double v, int k) {
+  switch (k) {
+    SRBD_BC16_CASE(0) SRBD_BC16_CASE(1) SRBD_BC16_CASE(2) SRBD_BC16_CASE(3)
+    SRBD_BC16_CASE(4) SRBD_BC16_CASE(5) SRBD_BC16_CASE(6) SRBD_BC16_CASE(7)
+    SRBD_BC16_CASE(8) SRBD_BC16_CASE(9) SRBD_BC16_CASE(10) SRBD_BC16_CASE(11)
+    default: return v;
+  }
+}
+
+// 1/d: v_rcp_f64 refined by two Newton steps (a correctly-rounded division costs ~10 dependent
+// instructions on the critical path of the sweep)
+__device__ __forceinline__ double rcp_nr(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  y = fma(y, fma(-d, y, 1.0), y);
+  return fma(y, fma(-d, y, 1.0), y);
+}
+
+// LDS hand-off between lanes of ONE wavefront: DS ops of a wave complete in order, so only the
+// compiler must be kept from reordering; the wait also drains outstanding LDS ops.
+__device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// (j + 6) mod 12: swaps the (euler, position) and (omega, velocity) halves of the SRBD state
+__device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
+
+// In-place symmetric sweep of a 12x12 SPD block held one row per lane (row r in lane r of a
+// 16-lane DPP row; lanes 12..15 shadow row 11): afterwards Sr = -(row r of the inverse).
+// Pivot k: a_rj <- a_rj - a_rk a_kj / d (r != k), a_kj <- a_kj / d, a_rk <- a_rk / d,
+// a_kk <- -1/d, written as fma(coef, a_kj, sc * a_rj) with (coef, sc) = (-a_rk/d, 1) off the pivot
+// row and (1/d, 0) on it; the pivot row a_k* is broadcast with v_mov_b64_dpp row_newbcast.
+__device__ __forceinline__ void sweep12(double (&Sr)[12], int r) {
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    double pk[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) pk[j] = bc16(Sr[j], k);
+    const double id = rcp_nr(pk[k]);
+    const bool piv = (r == k);
+    const double ark = Sr[k];
+    const double coef = piv ? id : -ark * id;
+    const double sc = piv ? 0.0 : 1.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+      if (j != k) Sr[j] = fma(coef, pk[j], sc * Sr[j]);
+    Sr[k] = piv ? -id : ark * id;
+  }
+}
 
 // packed-lower index -> (row, col), computed without loops
 __device__ inline void tri_rc(int e, int& r, int& c) {
@@ -50,28 +102,44 @@ __device__ inline void tri_rc(int e, int& r, int& c) {
   c = e - r * (r + 1) / 2;
 }
 
+template <int NT>  // NT > 0: horizon fixed at compile time (all trip counts constant); 0: runtime
 struct FastCtx {
-  int N, nz, m, p, lane;
+  int N_, lane;
   double *Md, *Nd, *Cd, *Gd, *K0, *K1, *Pd, *IX, *Hu, *SG, *PH, *DV, *X, *S, *Z, *Y, *RX, *RS, *RE, *WD,
-      *DI, *VV, *R1T, *TV, *QV, *WV, *DS, *DZ, *DY, *SC;
+      *DI, *VV, *TV, *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
+  PROF_DECL
   // Hu: [H_u (12) | H_x (12)] ; SG: [gamma6, psi8, gamma9, psi11, phi6, phi9, e6, e9]
 
+  // coupling block seen by group g: C (g = 0) or pi C^T pi^T (g = 1), entry (c, b)
+  __device__ double cg(int g, int c, int b) const { return Cd[g ? perm12(b) * 12 + perm12(c) : c * 12 + b]; }
+
+  // 12-term dot products as three independent 4-term chains (FP64 FMA latency)
   __device__ double dotrow12(const double* row, const double* v) const {  // sum_j row[j] v[j]
-    double a = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) a += row[j] * v[j];
-    return a;
+    for (int j = 0; j < 4; ++j) {
+      a0 += row[j] * v[j];
+      a1 += row[j + 4] * v[j + 4];
+      a2 += row[j + 8] * v[j + 8];
+    }
+    return (a0 + a1) + a2;
   }
   __device__ double dotcol12(const double* mat, int col, const double* v) const {  // sum_r mat[r][col] v[r]
-    double a = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
-    for (int r = 0; r < 12; ++r) a += mat[r * 12 + col] * v[r];
-    return a;
+    for (int r = 0; r < 4; ++r) {
+      a0 += mat[r * 12 + col] * v[r];
+      a1 += mat[(r + 4) * 12 + col] * v[r + 4];
+      a2 += mat[(r + 8) * 12 + col] * v[r + 8];
+    }
+    return (a0 + a1) + a2;
   }
 
   // --------------------------------------------------------------------- residuals ----
   __device__ double residuals() {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    (void)nz; (void)m; (void)p;
     for (int c = lane; c < nz; c += 64) {
       double v;
       if (c < 12 * N) {
@@ -119,6 +187,8 @@ struct FastCtx {
 
   // -------------------------------------------------------------------- factorise ----
   __device__ void factor() {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    (void)nz; (void)m; (void)p;
     for (int q = lane; q < m; q += 64) {
       const double w = (1.0 / S[q]) * Z[q] + kDelta;
       WD[q] = w;
@@ -174,52 +244,112 @@ struct FastCtx {
       DV[e] = v;
     }
     __syncthreads();
-    int r0, c0, r1 = 0, c1 = 0;
-    const int e0 = lane, e1 = lane + 64;
-    tri_rc(e0 < 78 ? e0 : 0, r0, c0);
-    if (e1 < 78) tri_rc(e1, r1, c1);
-    for (int i = 0; i < N; ++i) {
-      double* Di = DV + 78 * i;
-      if (i >= 1) {  // D_i = S_ii - C D_{i-1}^-1 C^T
-        const double* Dp = DV + 78 * (i - 1);
-        for (int e = lane; e < 144; e += 64) {
-          const int r = e / 12, c = e % 12;
-          double u = 0.0;
+    PROF_ADD(1);
+    // Twisted ("burn at both ends") block recursion, register-resident, one row per lane:
+    //   group 0 (lanes 0..15)  forward  D_i = S_ii - C D_{i-1}^-1 C^T        i = 0 .. mid-1
+    //   group 1 (lanes 16..31) backward E_j = S_jj - C^T E_{j+1}^-1 C        j = N-1 .. mid+1
+    //   middle (group 0)       T = S_mm - C D_{mid-1}^-1 C^T - C^T E_{mid+1}^-1 C
+    // Group 1 works in coordinates permuted by pi(j) = (j+6) % 12, where pi C^T pi^T has exactly
+    // C's sparsity, so both groups run the SAME instructions (16-lane DPP rows broadcast within
+    // each group). Each 12x12 SPD block is inverted by a symmetric sweep on lanes' rows; blocks are
+    // stored (original coordinates, packed lower) in DV for the solves.
+    {
+      const int mid = N / 2, nf = mid, nb = N - 1 - mid;
+      const int T = nf > nb ? nf : nb;
+      if (lane < 32) {
+        const int g = lane >> 4;
+        const int r = (lane & 15) < 12 ? (lane & 15) : 11;
+        const bool own = (lane & 15) < 12;
+        const int pr = g ? perm12(r) : r;
+        const int cnt = g ? nb : nf;
+        double* Vs = SC + 144 * g;   // per-group scratch for V = D^-1 Cg^T
+        double* XB = SC + 288;       // group 1's C^T E^-1 C (permuted) for the middle block
+        double Dr[12];
+#pragma unroll 1
+        for (int t = 0; t <= T; ++t) {
+          const bool mstep = (t == T);
+          const int i = mstep ? mid : (g ? N - 1 - t : t);
+          const bool act = mstep ? (g == 0 || nb >= 1) : (t < cnt);
+          const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+          double Sr[12];
+          if (act) {
+            const double* Si = DV + 78 * i;
 #pragma unroll
-          for (int k = 0; k < 12; ++k) u += Cd[r * 12 + k] * Dp[sym_idx(k, c)];
-          SC[e] = u;
+            for (int c = 0; c < 12; ++c) Sr[c] = Si[sym_idx(pr, g ? perm12(c) : c)];
+            if (prev) {
+              // V = D^-1 Cg^T (row r); Cg = C (group 0) or pi C^T pi^T (group 1), C's pattern:
+              // row c has {c} U {6,7,8} (c < 3) U {c+6} (3 <= c < 6)
+              double V[12];
+#pragma unroll
+              for (int c = 0; c < 12; ++c) {
+                double v = Dr[c] * cg(g, c, c);
+                if (c < 3) v += Dr[6] * cg(g, c, 6) + Dr[7] * cg(g, c, 7) + Dr[8] * cg(g, c, 8);
+                else if (c < 6) v += Dr[c + 6] * cg(g, c, c + 6);
+                V[c] = v;
+              }
+              lds_wave_sync();
+              if (own) {
+#pragma unroll
+                for (int c = 0; c < 12; ++c) Vs[r * 12 + c] = V[c];
+              }
+              lds_wave_sync();
+              // X = Cg V (row r): rows a in nz(Cg row r)
+              double X[12];
+              const double cr = cg(g, r, r);
+#pragma unroll
+              for (int c = 0; c < 12; ++c) X[c] = cr * Vs[r * 12 + c];
+              if (r < 3) {
+                const double c6 = cg(g, r, 6), c7 = cg(g, r, 7), c8 = cg(g, r, 8);
+#pragma unroll
+                for (int c = 0; c < 12; ++c) X[c] += c6 * Vs[72 + c] + c7 * Vs[84 + c] + c8 * Vs[96 + c];
+              } else if (r < 6) {
+                const double c9 = cg(g, r, r + 6);
+#pragma unroll
+                for (int c = 0; c < 12; ++c) X[c] += c9 * Vs[(r + 6) * 12 + c];
+              }
+              if (mstep && g == 1) {
+                if (own) {
+#pragma unroll
+                  for (int c = 0; c < 12; ++c) XB[r * 12 + c] = X[c];
+                }
+              } else {
+#pragma unroll
+                for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
+              }
+            }
+          }
+          if (mstep) {
+            lds_wave_sync();
+            if (g == 0 && nb >= 1) {  // un-permute group 1's term: X_b[r][c] = XB[pi r][pi c]
+#pragma unroll
+              for (int c = 0; c < 12; ++c) Sr[c] -= XB[perm12(r) * 12 + perm12(c)];
+            }
+          }
+          if (act && !(mstep && g == 1)) {
+            sweep12(Sr, r);
+#pragma unroll
+            for (int c = 0; c < 12; ++c) Dr[c] = -Sr[c];
+            if (own) {
+              double* Di = DV + 78 * i;
+#pragma unroll
+              for (int c = 0; c < 12; ++c) {
+                const int pc = g ? perm12(c) : c;
+                if (pc <= pr) Di[pr * (pr + 1) / 2 + pc] = Dr[c];
+              }
+            }
+          }
         }
-        __syncthreads();
-        for (int e = lane; e < 78; e += 64) {
-          int r, c;
-          tri_rc(e, r, c);
-          Di[e] -= dotrow12(SC + 12 * r, Cd + 12 * c);
-        }
-        __syncthreads();
       }
-      for (int k = 0; k < 12; ++k) {  // symmetric sweep -> -D_i^-1
-        const double id = 1.0 / Di[k * (k + 1) / 2 + k];
-        const double a0 = Di[e0], k0r = Di[sym_idx(r0, k)], k0c = Di[sym_idx(c0, k)];
-        double a1 = 0.0, k1r = 0.0, k1c = 0.0;
-        if (e1 < 78) { a1 = Di[e1]; k1r = Di[sym_idx(r1, k)]; k1c = Di[sym_idx(c1, k)]; }
-        __syncthreads();
-        if (e0 < 78) {
-          Di[e0] = (r0 != k && c0 != k) ? a0 - k0r * k0c * id : ((r0 == k && c0 == k) ? -id : a0 * id);
-        }
-        if (e1 < 78) {
-          Di[e1] = (r1 != k && c1 != k) ? a1 - k1r * k1c * id : ((r1 == k && c1 == k) ? -id : a1 * id);
-        }
-        __syncthreads();
-      }
-      if (e0 < 78) Di[e0] = -Di[e0];
-      if (e1 < 78) Di[e1] = -Di[e1];
-      __syncthreads();
     }
+    __syncthreads();
+    PROF_ADD(2);
   }
 
   // ------------------------------------------------------------------------ solve ----
   // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
   __device__ void solve(int mode, double smu) {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    (void)nz; (void)m; (void)p;
     for (int q = lane; q < m; q += 64) {
       const double si = 1.0 / S[q];
       double r2 = -(si * (S[q] * Z[q]));
@@ -227,40 +357,37 @@ struct FastCtx {
       VV[q] = DI[q] * (r2 + WD[q] * RS[q]);
     }
     __syncthreads();
-    for (int c = lane; c < nz; c += 64) {
-      double v = -RX[c];
-      if (c >= 12 * N) {
-        const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
-        double g = 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) g += Gd[k * 12 + j] * VV[16 * i + k];
-        v -= g;
-      }
-      R1T[c] = v;
-    }
-    __syncthreads();
-    for (int c = lane; c < 12 * N; c += 64) TV[c] = R1T[c] * IX[c % 12];
+    // t = Phi^-1 r1~ with r1~ = -RX - G^T VV; G only touches the foot columns {0,1,2,7 | 3,4,5,10},
+    // and each foot's columns only through that foot's 8 rows
+    for (int c = lane; c < 12 * N; c += 64) TV[c] = -RX[c] * IX[c % 12];
     for (int task = lane; task < 3 * N; task += 64) {
       if (task < 2 * N) {
-        const int i = task >> 1, f = task & 1;
+        const int i = task >> 1, f = task & 1, b = 12 * N + 12 * i;
         const double* ph = PH + 20 * i + 10 * f;
+        const double* vv = VV + 16 * i + 8 * f;
         double rv[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) rv[a] = R1T[12 * N + 12 * i + c_tab.foot_col[f][a]];
+        for (int a = 0; a < 4; ++a) {
+          const int col = c_tab.foot_col[f][a];
+          double gv = 0.0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv += Gd[(8 * f + k) * 12 + col] * vv[k];
+          rv[a] = -RX[b + col] - gv;
+        }
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * rv[b];
-          TV[12 * N + 12 * i + c_tab.foot_col[f][a]] = t;
+          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * rv[q];
+          TV[b + c_tab.foot_col[f][a]] = t;
         }
       } else {
         const int i = task - 2 * N, b = 12 * N + 12 * i;
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
-        TV[b + 6] = (kDelta * R1T[b + 6] + SG[6] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
-        TV[b + 9] = (kDelta * R1T[b + 9] + SG[7] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
-        TV[b + 8] = R1T[b + 8] * SG[1];
-        TV[b + 11] = R1T[b + 11] * SG[3];
+        TV[b + 6] = (kDelta * -RX[b + 6] + SG[6] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
+        TV[b + 9] = (kDelta * -RX[b + 9] + SG[7] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
+        TV[b + 8] = -RX[b + 8] * SG[1];
+        TV[b + 11] = -RX[b + 11] * SG[3];
       }
     }
     __syncthreads();
@@ -272,34 +399,104 @@ struct FastCtx {
       QV[e] = v + RE[e];
     }
     __syncthreads();
-    for (int i = 0; i < N; ++i) {  // forward: q_i -= C w_{i-1}; w_i = D_i^-1 q_i
-      if (i >= 1) {
-        if (lane < 12) QV[12 * i + lane] -= dotrow12(Cd + 12 * lane, WV + 12 * (i - 1));
-        __syncthreads();
-      }
-      if (lane < 12) {
-        const double* Di = DV + 78 * i;
-        double acc = 0.0;
+    PROF_ADD(3);
+    // Twisted block solve of (A_dyn Phi^-1 A_dyn^T + dI) y = g with the factors of factor():
+    //   elimination: group 0  q_i = g_i - C w_{i-1},   w_i = D_i^-1 q_i     (i = 0 .. mid-1)
+    //                group 1  p_j = g_j - C^T v_{j+1}, v_j = E_j^-1 p_j     (j = N-1 .. mid+1)
+    //   middle:      y_mid = T^-1 (g_mid - C w_{mid-1} - C^T v_{mid+1})
+    //   outward:     group 0  y_i = w_i - D_i^-1 C^T y_{i+1};  group 1  y_j = v_j - E_j^-1 C y_{j-1}
+    // (group 1 in pi-permuted coordinates, so both groups run the same instructions).
+    // g is read from QV, the solution y is written back to QV; w / v are kept in WV.
+    {
+      const int mid = N / 2, nf = mid, nb = N - 1 - mid;
+      const int T = nf > nb ? nf : nb;
+      if (lane < 32) {
+        const int g = lane >> 4;
+        const int r = (lane & 15) < 12 ? (lane & 15) : 11;
+        const bool own = (lane & 15) < 12;
+        const int pr = g ? perm12(r) : r;
+        const int cnt = g ? nb : nf;
+        double Crow[12], Ccol[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * QV[12 * i + k];
-        WV[12 * i + lane] = acc;
+        for (int j = 0; j < 12; ++j) {
+          Crow[j] = cg(g, r, j);
+          Ccol[j] = cg(g, j, r);
+        }
+        double w = 0.0;
+#pragma unroll 1
+        for (int t = 0; t <= T; ++t) {
+          const bool mstep = (t == T);
+          const int i = mstep ? mid : (g ? N - 1 - t : t);
+          const bool act = mstep ? (g == 0 || nb >= 1) : (t < cnt);
+          const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+          double cw = 0.0;  // Cg times the previous w (both groups)
+          if (act && prev) {
+            double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              c0 += Crow[j] * bc16(w, j);
+              c1 += Crow[j + 4] * bc16(w, j + 4);
+              c2 += Crow[j + 8] * bc16(w, j + 8);
+            }
+            cw = (c0 + c1) + c2;
+          }
+          if (mstep) {  // group 1 hands C^T v_{mid+1} (original coordinates) to group 0
+            if (g == 1 && own && nb >= 1) SC[432 + pr] = cw;
+            lds_wave_sync();
+          }
+          if (act && !(mstep && g == 1)) {
+            const double* Di = DV + 78 * i;
+            double Dr[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12(k) : k)];
+            double q = QV[12 * i + pr] - cw;
+            if (mstep && nb >= 1) q -= SC[432 + r];
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              a0 += Dr[k] * bc16(q, k);
+              a1 += Dr[k + 4] * bc16(q, k + 4);
+              a2 += Dr[k + 8] * bc16(q, k + 8);
+            }
+            w = (a0 + a1) + a2;
+            if (own) WV[12 * i + pr] = w;
+          }
+        }
+        // outward substitution from the middle block (y_mid = group 0's last w, also in WV_mid)
+        lds_wave_sync();
+        if (own && g == 0) QV[12 * mid + r] = w;
+        double y = (g == 0) ? w : WV[12 * mid + pr];
+#pragma unroll 1
+        for (int t = 0; t < T; ++t) {
+          const int i = g ? mid + 1 + t : mid - 1 - t;
+          if (t < cnt) {
+            const double* Di = DV + 78 * i;
+            double Dr[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12(k) : k)];
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // Cg^T y_prev
+              s0 += Ccol[j] * bc16(y, j);
+              s1 += Ccol[j + 4] * bc16(y, j + 4);
+              s2 += Ccol[j + 8] * bc16(y, j + 8);
+            }
+            const double sc = (s0 + s1) + s2;
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              a0 += Dr[k] * bc16(sc, k);
+              a1 += Dr[k + 4] * bc16(sc, k + 4);
+              a2 += Dr[k + 8] * bc16(sc, k + 8);
+            }
+            y = WV[12 * i + pr] - ((a0 + a1) + a2);
+            if (own) QV[12 * i + pr] = y;
+          }
+        }
       }
-      __syncthreads();
     }
-    if (lane < 12) QV[12 * (N - 1) + lane] = WV[12 * (N - 1) + lane];
     __syncthreads();
-    for (int i = N - 2; i >= 0; --i) {  // backward: y_i = w_i - D_i^-1 C^T y_{i+1}
-      if (lane < 12) SC[lane] = dotcol12(Cd, lane, QV + 12 * (i + 1));
-      __syncthreads();
-      if (lane < 12) {
-        const double* Di = DV + 78 * i;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * SC[k];
-        QV[12 * i + lane] = WV[12 * i + lane] - acc;
-      }
-      __syncthreads();
-    }
+    PROF_ADD(4);
     for (int c = lane; c < 12 * N; c += 64) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int k = c / 12 + 1, j = c % 12;
       double aty = Pd[j] * QV[12 * (k - 1) + j];
@@ -332,7 +529,7 @@ struct FastCtx {
         TV[b + 9] -= SG[2] * a9;
         TV[b + 8] -= SG[1] * a8;
         TV[b + 11] -= SG[3] * a11;
-        const double rho6 = R1T[b + 6] - a6, rho9 = R1T[b + 9] - a9;
+        const double rho6 = -RX[b + 6] - a6, rho9 = -RX[b + 9] - a9;  // no G entries in cols 6, 9
         DY[12 * N + 2 * i] = (SG[6] * rho6 - SG[4] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
         DY[12 * N + 2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
       }
@@ -347,9 +544,12 @@ struct FastCtx {
       DS[q] = -RS[q] - gd + kDelta * dz;
     }
     __syncthreads();
+    PROF_ADD(3);
   }
 
   __device__ double step_length(const double* v, const double* dv) const {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    (void)nz; (void)m; (void)p;
     double mn = INFINITY;
     for (int q = lane; q < m; q += 64) {
       const bool c = dv[q] < 0.0;
@@ -361,22 +561,24 @@ struct FastCtx {
   }
 };
 
+template <int NT>
 __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = blockIdx.x;
   if (env >= args.batch) return;
-  const int N = args.N, lane = threadIdx.x;
+  const int N = NT > 0 ? NT : args.N, lane = threadIdx.x;
   const FastLayout Lo(N);
-  FastCtx C;
-  C.N = N; C.nz = 24 * N; C.m = 16 * N; C.p = 14 * N; C.lane = lane;
+  FastCtx<NT> C;
+  C.N_ = N;
+  C.lane = lane;
   C.Md = smem + Lo.Md; C.Nd = smem + Lo.Nd; C.Cd = smem + Lo.Cd; C.Gd = smem + Lo.Gd;
   C.K0 = smem + Lo.K0; C.K1 = smem + Lo.K1; C.Pd = smem + Lo.Pd; C.IX = smem + Lo.IX;
   C.Hu = smem + Lo.Hu; C.SG = smem + Lo.SG; C.PH = smem + Lo.PH; C.DV = smem + Lo.DV;
   C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
   C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE; C.WD = smem + Lo.WD; C.DI = smem + Lo.DI;
-  C.VV = smem + Lo.VV; C.R1T = smem + Lo.R1T; C.TV = smem + Lo.TV; C.QV = smem + Lo.QV; C.WV = smem + Lo.WV;
+  C.VV = smem + Lo.VV; C.TV = smem + Lo.TV; C.QV = smem + Lo.QV; C.WV = smem + Lo.WV;
   C.DS = smem + Lo.DS; C.DZ = smem + Lo.DZ; C.DY = smem + Lo.DY; C.SC = smem + Lo.SC;
-  const int nz = C.nz, m = C.m, p = C.p, nA = nnz_A(N), nG = 28 * N;
+  const int nz = 24 * N, m = 16 * N, p = 14 * N, nA = nnz_A(N), nG = 28 * N;
   const double* Hg = solver_in(args, 0) + (size_t)env * nz;
   const double* Gg = solver_in(args, 1) + (size_t)env * nG;
   const double* Ag = solver_in(args, 2) + (size_t)env * nA;
@@ -479,8 +681,10 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   __syncthreads();
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
+  PROF_MARK_CTX(C);
   for (int it = 0; it < args.n_iter; ++it) {
     const double mu = C.residuals();
+    PROF_ADD_CTX(C, 0);
     C.factor();
     C.solve(0, 0.0);
     const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
@@ -489,6 +693,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
     const double mu_aff = wave_sum(sza) / m;
     const double sigma = pow(mu_aff / mu, 3.0);
     __syncthreads();
+    PROF_ADD_CTX(C, 5);
     C.solve(1, sigma * mu * 1.0);
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
     __syncthreads();
@@ -513,7 +718,9 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
       res2 = sqrt(wave_sum(c));
     }
     __syncthreads();
+    PROF_ADD_CTX(C, 5);
   }
+  PROF_FLUSH(C);
   double* xo = solver_out(args, 0) + (size_t)env * nz;
   double* so = solver_out(args, 1) + (size_t)env * m;
   double* zo = solver_out(args, 2) + (size_t)env * m;

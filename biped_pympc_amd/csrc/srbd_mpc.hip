@@ -57,14 +57,21 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
-  static size_t cfg_general = 0, cfg_fast = 0;
+  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0;
   srbd::SolverArgs a = a0;
   a.only_flagged = 0;
   if (g_solver_path == 0) {
     const size_t lds = fast_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
-    if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_kernel, lds, &cfg_fast)) return rc;
-    hipLaunchKernelGGL(srbd::pdipm_srbd_kernel, dim3(a.batch), dim3(64), lds, s, a);
+    // horizon-specialised instantiations for the common horizons, runtime-N otherwise
+    const void* fn = a.N == 10 ? (const void*)srbd::pdipm_srbd_kernel<10>
+                   : a.N == 20 ? (const void*)srbd::pdipm_srbd_kernel<20>
+                               : (const void*)srbd::pdipm_srbd_kernel<0>;
+    size_t* cfg = a.N == 10 ? &cfg_fast10 : a.N == 20 ? &cfg_fast20 : &cfg_fast;
+    if (int rc = ensure_lds_attr(fn, lds, cfg)) return rc;
+    if (a.N == 10) hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<10>, dim3(a.batch), dim3(64), lds, s, a);
+    else if (a.N == 20) hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<20>, dim3(a.batch), dim3(64), lds, s, a);
+    else hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<0>, dim3(a.batch), dim3(64), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_kernel launch");
     a.only_flagged = 1;  // general kernel picks up the QPs that are not stage-invariant
@@ -112,6 +119,16 @@ int srbd_abi_version(void) { return SRBD_ABI_VERSION; }
 const char* srbd_last_error(void) { return g_last_error.c_str(); }
 
 size_t srbd_solver_lds_bytes(int horizon) { return horizon_ok(horizon) ? solver_lds_bytes(horizon) : 0; }
+
+#ifdef SRBD_PHASE_PROF
+// diagnostic build only: read and reset the per-phase cycle accumulators
+int srbd_debug_phase_cycles(unsigned long long* out16) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(srbd::g_phase_cycles), 16 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_phase_cycles), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int srbd_set_solver_path(int path) {
   if (path != 0 && path != 1) return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto) or 1 (general)");

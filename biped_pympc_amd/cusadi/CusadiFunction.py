@@ -74,8 +74,8 @@ class CusadiFunction:
         lin = self._dense_index[out_idx]
         s1, s2 = fn.size1_out(out_idx), fn.size2_out(out_idx)
         dense = torch.zeros((self.num_instances, s1 * s2), device=self._device, dtype=torch.double)
-        dense.index_put_((slice(None), lin), self.outputs_sparse[out_idx].reshape(self.num_instances, -1),
-                         accumulate=True)
+        # sums duplicates like the reference's sparse_coo_tensor(...).to_dense() (there are none)
+        dense.index_add_(1, lin, self.outputs_sparse[out_idx].reshape(self.num_instances, -1))
         return dense.view(self.num_instances, s1, s2)
 
     def checkInputDimensions(self, inputs):
