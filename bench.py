@@ -147,7 +147,7 @@ def main():
         achieved = flops / (ms_pdipm * 1e-3) / 1e12
         traffic, traffic_src = load_pmc(N, B, K)
         roofline = {
-            "bound": "mfma", "kernel": "pdipm_kernel", "achieved": round(achieved, 4),
+            "bound": "mfma", "kernel": f"pdipm_srbd_kernel<{N if N in (10, 20) else 0}>", "achieved": round(achieved, 4),
             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
             "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_pdipm, 4),
