@@ -79,11 +79,13 @@ def check(rc: int, what: str) -> None:
 
 
 class solver_path:
-    """Context manager selecting the solver kernels: "auto" (fast stage-invariant kernel +
-    general fallback) or "general" (general kernel only). Process-wide; for tests/benchmarks."""
+    """Context manager selecting the solver kernels: "auto" (stage-invariant kernels -- the
+    register-resident one at N = 10 -- plus the general fallback), "general" (general kernel only)
+    or "lds" (the LDS-resident stage-invariant kernel at every horizon). Process-wide; for
+    tests/benchmarks."""
 
     def __init__(self, path: str):
-        self.code = {"auto": 0, "general": 1}[path]
+        self.code = {"auto": 0, "general": 1, "lds": 2}[path]
 
     def __enter__(self):
         check(lib().srbd_set_solver_path(self.code), "srbd_set_solver_path")

@@ -1,0 +1,798 @@
+// pdipm_srbd_reg.hpp -- register-resident variant of the stage-invariant PDIPM kernel.
+//
+// Same algorithm, inputs and outputs as pdipm_srbd_kernel (pdipm_srbd.hpp; reference
+// biped_pympc/casadi/sparse_pdipm_solver.py:357-534), re-laid out so that one QP needs <= 20 KiB of
+// LDS at N = 10 and a CU holds 8 QPs = 2 waves per SIMD (the one-wave-per-SIMD kernel spends ~43% of
+// its wave cycles parked on LDS latency; profiles/r01/). What moved out of LDS:
+//   * the inequality-indexed vectors s, w = z/s + delta, D^-1 = 1/(1 + delta w), ds, dz, r_s live in
+//     registers of the lane that owns row q = lane + 64 t (z keeps an LDS mirror for G^T z);
+//   * the x-column part of r_x and the dynamics part of r_e live in registers of their owner lane;
+//   * M (24 nonzeros), C = M diag(P / phi_x) (24, plus its pi-permuted transpose for the backward
+//     group) and G (16 rows x 4 foot columns) are stored compactly;
+//   * the two 4x4 foot inverses of Phi_u stay in the registers of their task lane;
+//   * the block-recursion exchanges (rows of V = D^-1 C^T, the backward group's middle term, the
+//     middle-vector hand-offs) go through DPP / ds_bpermute instead of LDS scratch, and the solve
+//     chains keep w / v in registers (horizon is compile-time, chains fully unrolled).
+// Compact M layout (same for C): [0..11] diag, [12 + 3r + k] = (r, 6 + k) for r < 3,
+// [21 + r - 3] = (r, r + 6) for 3 <= r < 6 -- exactly the stage-coupling sparsity of -A_d.
+#pragma once
+#include "pdipm_srbd.hpp"
+
+namespace srbd {
+
+template <int N>
+struct RegLayout {
+  static constexpr int nz = 24 * N, m = 16 * N, p = 14 * N, nx = 12 * N;
+  static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 144, K0 = Gf + 64, K1 = K0 + 78,
+                       Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, DV = SG + 16,
+                       X = DV + 78 * N, Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
+                       QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N, total = DYm + 2 * N;
+  static constexpr int SI = (m + 63) / 64, SE = (p + 63) / 64, SX = (nx + 63) / 64;
+  static_assert((DV & 1) == 0 && (X & 1) == 0 && (TV & 1) == 0, "16-byte aligned vectors");
+};
+
+// foot of u column j ({0,1,2,7} left, {3,4,5,10} right, else -1), its position, and the inverse
+__device__ __forceinline__ int foot_of(int j) { return (j < 3 || j == 7) ? 0 : ((j < 6 || j == 10) ? 1 : -1); }
+__device__ __forceinline__ int foot_pos(int j) { return j < 6 ? j % 3 : 3; }
+__host__ __device__ constexpr int foot_colj(int f, int a) { return a < 3 ? a + 3 * f : 7 + 3 * f; }
+__host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6; }
+
+// lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
+__device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
+
+// element (c, b) of a compact M / C block (c or b runtime)
+__device__ __forceinline__ double cel(const double* cc, int c, int b) {
+  if (b == c) return cc[c];
+  if (c < 3 && b >= 6 && b < 9) return cc[12 + 3 * c + b - 6];
+  if (c >= 3 && c < 6 && b == c + 6) return cc[21 + c - 3];
+  return 0.0;
+}
+// (M v)_r and (M^T v)_j from the compact block
+__device__ __forceinline__ double mrow(const double* mc, int r, const double* v) {
+  double a = mc[r] * v[r];
+  if (r < 3) a += (mc[12 + 3 * r] * v[6] + mc[13 + 3 * r] * v[7]) + mc[14 + 3 * r] * v[8];
+  else if (r < 6) a += mc[21 + r - 3] * v[r + 6];
+  return a;
+}
+__device__ __forceinline__ double mcol(const double* mc, int j, const double* v) {
+  double a = mc[j] * v[j];
+  if (j >= 6 && j < 9) a += (mc[12 + j - 6] * v[0] + mc[15 + j - 6] * v[1]) + mc[18 + j - 6] * v[2];
+  else if (j >= 9) a += mc[21 + j - 9] * v[j - 6];
+  return a;
+}
+// dense 12-term row / column products (N block)
+__device__ __forceinline__ double drow12(const double* row, const double* v) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a0 += row[j] * v[j];
+    a1 += row[j + 4] * v[j + 4];
+    a2 += row[j + 8] * v[j + 8];
+  }
+  return (a0 + a1) + a2;
+}
+__device__ __forceinline__ double dcol12(const double* mat, int col, const double* v) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    a0 += mat[r * 12 + col] * v[r];
+    a1 += mat[(r + 4) * 12 + col] * v[r + 4];
+    a2 += mat[(r + 8) * 12 + col] * v[r + 8];
+  }
+  return (a0 + a1) + a2;
+}
+// (G xu)_k over the 4 columns of row k's foot
+__device__ __forceinline__ double grow4(const double* gf, int k, const double* xu) {
+  const int f = k >> 3;
+  const double* g = gf + 4 * k;
+  return (g[0] * xu[foot_colj(f, 0)] + g[1] * xu[foot_colj(f, 1)]) +
+         (g[2] * xu[foot_colj(f, 2)] + g[3] * xu[foot_colj(f, 3)]);
+}
+
+template <int N>
+struct RegCtx {
+  using Lo = RegLayout<N>;
+  static constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx;
+  static constexpr int SI = Lo::SI, SE = Lo::SE, SX = Lo::SX;
+  static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
+  double* L;
+  int lane;
+  const double *fg, *hg, *bg;
+  double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
+  PROF_DECL
+
+  __device__ double* at(int off) const { return L + off; }
+  // The lane index, re-materialised as an opaque value at the start of every phase: keeps the
+  // compiler from hoisting each phase's per-lane addresses and predicates out of the Newton loop
+  // (that alone pinned > 100 registers for the whole solve).
+  __device__ int fresh_lane() const {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    return l;
+  }
+
+  // --------------------------------------------------------------------- residuals ----
+  __device__ double residuals() {
+    const int lane = fresh_lane();
+    const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
+                 *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
+    double *RXu = at(Lo::RXu), *REm = at(Lo::REm);
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
+      const int c = lane + 64 * t;
+      if (c < nx) {
+        const int k = c / 12 + 1, j = c % 12;
+        const double v = Hu[12 + j] * X[c] + fg[c];
+        double ay = Pd[j] * Y[12 * (k - 1) + j];
+        if (k < N) ay += mcol(Mc, j, Y + 12 * k);
+        rxx[t] = v + ay;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // r_x, u columns: H_u u + f + G^T z + N^T y + e-rows (LDS)
+      const int c = lane + 64 * t;
+      if (c < nx) {
+        const int i = c / 12, j = c % 12;
+        const double v = Hu[j] * X[nx + c] + fg[nx + c];
+        double gz = 0.0;
+        const int f = foot_of(j);
+        if (f >= 0) {
+          const int a = foot_pos(j);
+          const double* zf = Z + 16 * i + 8 * f;
+          const double* g = Gf + 32 * f + a;
+          double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            g0 += g[4 * k] * zf[k];
+            g1 += g[4 * (k + 4)] * zf[k + 4];
+          }
+          gz = g0 + g1;
+        }
+        double ay = dcol12(Nd, j, Y + 12 * i);
+        if (j == 6) ay += SG[6] * Y[nx + 2 * i];
+        if (j == 9) ay += SG[7] * Y[nx + 2 * i + 1];
+        RXu[c] = (v + gz) + ay;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < SE; ++t) {  // r_e = A x - b (owner regs; x-moment rows also in LDS)
+      const int e = lane + 64 * t;
+      if (e < p) {
+        double v;
+        if (e < nx) {
+          const int i = e / 12, r = e % 12;
+          v = (i >= 1) ? mrow(Mc, r, X + 12 * (i - 1)) : 0.0;
+          v += Pd[r] * X[12 * i + r];
+          v += drow12(Nd + 12 * r, X + nx + 12 * i);
+        } else {
+          const int i = (e - nx) / 2, w = (e - nx) % 2;
+          v = SG[6 + w] * X[nx + 12 * i + (w ? 9 : 6)];
+        }
+        re[t] = v - bg[e];
+        if (e >= nx) REm[e - nx] = re[t];
+      }
+    }
+    double sz = 0.0;
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // r_s = G u + s - h (owner regs)
+      const int q = lane + 64 * t;
+      if (q < m) {
+        const int i = q / 16, k = q % 16;
+        const double v = grow4(Gf, k, X + nx + 12 * i);
+        rs[t] = (v + s[t]) - hg[q];
+        sz += s[t] * z[t];
+      }
+    }
+    __syncthreads();
+    return wave_sum(sz) / m;
+  }
+
+  // -------------------------------------------------------------------- factorise ----
+  __device__ void factor() {
+    const int lane = fresh_lane();
+    double *VV = at(Lo::VV), *DV = at(Lo::DV), *PHs = at(Lo::TV);  // PHs: scratch, TV is dead here
+    const double *Gf = at(Lo::Gf), *Hu = at(Lo::Hu), *Nd = at(Lo::Nd), *K0 = at(Lo::K0), *K1 = at(Lo::K1);
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + 64 * t;
+      if (q < m) {
+        wd[t] = (1.0 / s[t]) * z[t] + kDelta;
+        di[t] = 1.0 / (1.0 + kDelta * wd[t]);
+        VV[q] = di[t] * wd[t];  // Lambda, shared with the foot tasks
+      }
+    }
+    __syncthreads();
+    if (lane < 2 * N) {  // foot blocks of Phi_u, inverted; kept in this lane's registers
+      const int i = lane >> 1, f = lane & 1;
+      double a[10];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? Hu[foot_colj(f, r)] + kBeta : 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double lam = VV[16 * i + 8 * f + k];
+        const double* g4 = Gf + 4 * (8 * f + k);
+        double gl[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) gl[b] = g4[b];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * gl[r] * gl[c];
+      }
+      sweep_inverse<4>(a);
+#pragma unroll
+      for (int e = 0; e < 10; ++e) {
+        ph[e] = a[e];
+        PHs[20 * i + 10 * f + e] = a[e];
+      }
+    }
+    __syncthreads();
+    for (int e = lane; e < 78 * N; e += 64) {  // S_ii = K + sum_f N_f Phi_f^-1 N_f^T
+      const int i = e / 78, l = e % 78;
+      int r, c;
+      tri_rc(l, r, c);
+      double v = (i == 0 ? K0 : K1)[l];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const double* ph_ = PHs + 20 * i + 10 * f;
+        double vc[4], vr[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          vr[a] = Nd[r * 12 + foot_colj(f, a)];
+          vc[a] = Nd[c * 12 + foot_colj(f, a)];
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) t += ph_[sym_idx(a, b)] * vc[b];
+          v += vr[a] * t;
+        }
+      }
+      DV[e] = v;
+    }
+    __syncthreads();
+    PROF_ADD(1);
+    // Twisted block recursion (see pdipm_srbd.hpp FastCtx::factor): group 0 (lanes 0..15) forward,
+    // group 1 (lanes 16..31) backward in pi-permuted coordinates, middle block by group 0. Row r of
+    // V = D^-1 Cg^T is computed by lane r; X = Cg V needs rows {r, 6, 7, 8} (r < 3) or {r, r + 6}
+    // (3 <= r < 6), fetched with row_newbcast / row_shl:6 DPP; group 1's middle term reaches
+    // group 0 through ds_bpermute.
+    if (lane < 32) {
+      const int g = lane >> 4, l16 = lane & 15;
+      const int r = l16 < 12 ? l16 : 11;
+      const bool own = l16 < 12;
+      const int pr = g ? perm12(r) : r;
+      const int cnt = g ? nb : nf;
+      const double* cc = at(Lo::Cc) + 24 * g;
+      const double crd = cc[r];
+      const double cra0 = r < 3 ? cc[12 + 3 * r] : 0.0, cra1 = r < 3 ? cc[13 + 3 * r] : 0.0,
+                   cra2 = r < 3 ? cc[14 + 3 * r] : 0.0;
+      const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
+      double Dr[12];
+#pragma unroll
+      for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
+#pragma unroll 1
+      for (int t = 0; t <= T; ++t) {
+        const bool mstep = (t == T);
+        const int i = mstep ? mid : (g ? N - 1 - t : t);
+        const bool act = mstep ? true : (t < cnt);
+        const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+        double Sr[12], X[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) X[c] = 0.0;
+        if (act) {
+          const double* Si = DV + 78 * i;
+#pragma unroll
+          for (int c = 0; c < 12; ++c) Sr[c] = Si[sym_idx(pr, g ? perm12c(c) : c)];
+          if (prev) {
+            double V[12];
+#pragma unroll
+            for (int c = 0; c < 12; ++c) {
+              double v = Dr[c] * cc[c];
+              if (c < 3) v += (Dr[6] * cc[12 + 3 * c] + Dr[7] * cc[13 + 3 * c]) + Dr[8] * cc[14 + 3 * c];
+              else if (c < 6) v += Dr[c + 6] * cc[21 + c - 3];
+              V[c] = v;
+            }
+#pragma unroll
+            for (int c = 0; c < 12; ++c) {
+              const double v = V[c];
+              X[c] = (crd * v + crb * shl6(v)) +
+                     ((cra0 * bc16(v, 6) + cra1 * bc16(v, 7)) + cra2 * bc16(v, 8));
+            }
+            if (!(mstep && g == 1)) {
+#pragma unroll
+              for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
+            }
+          }
+        }
+        if (mstep && nb >= 1) {  // X_b[r][c] = X'[pi r][pi c], held by lane 16 + pi(r)
+#pragma unroll
+          for (int c = 0; c < 12; ++c) {
+            const double xb = __shfl(X[perm12c(c)], 16 + perm12(r), 64);
+            if (g == 0) Sr[c] -= xb;
+          }
+        }
+        if (act && !(mstep && g == 1)) {
+          sweep12(Sr, r);
+#pragma unroll
+          for (int c = 0; c < 12; ++c) Dr[c] = -Sr[c];
+          if (own) {
+            double* Di = DV + 78 * i;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) {
+              const int pc = g ? perm12c(c) : c;
+              if (pc <= pr) Di[pr * (pr + 1) / 2 + pc] = Dr[c];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    PROF_ADD(2);
+  }
+
+  // ------------------------------------------------------------------------ solve ----
+  // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
+  __device__ void solve(int mode, double smu) {
+    const int lane = fresh_lane();
+    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
+    const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
+                 *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd),
+                 *DV = at(Lo::DV);
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + 64 * t;
+      if (q < m) {
+        const double si = 1.0 / s[t];
+        double r2 = -(si * (s[t] * z[t]));
+        if (mode) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
+        VV[q] = di[t] * (r2 + wd[t] * rs[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {
+      const int c = lane + 64 * t;
+      if (c < nx) TV[c] = -rxx[t] * IX[c % 12];
+    }
+    __syncthreads();
+    // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
+    if (lane < 3 * N) {
+      if (lane < 2 * N) {
+        const int i = lane >> 1, f = lane & 1, b = 12 * i;
+        const double* vv = VV + 16 * i + 8 * f;
+        double rv[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const double* g = Gf + 32 * f + a;
+          double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            g0 += g[4 * k] * vv[k];
+            g1 += g[4 * (k + 4)] * vv[k + 4];
+          }
+          rv[a] = -RXu[b + foot_colj(f, a)] - (g0 + g1);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * rv[q];
+          TV[nx + b + foot_colj(f, a)] = t;
+        }
+      } else {
+        const int i = lane - 2 * N, b = 12 * i;
+        const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
+        TV[nx + b + 6] = (kDelta * -RXu[b + 6] + SG[6] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
+        TV[nx + b + 9] = (kDelta * -RXu[b + 9] + SG[7] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
+        TV[nx + b + 8] = -RXu[b + 8] * SG[1];
+        TV[nx + b + 11] = -RXu[b + 11] * SG[3];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < SE; ++t) {  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
+      const int e = lane + 64 * t;
+      if (e < nx) {
+        const int i = e / 12, r = e % 12;
+        double v = (i >= 1) ? mrow(Mc, r, TV + 12 * (i - 1)) : 0.0;
+        v += Pd[r] * TV[12 * i + r];
+        v += drow12(Nd + 12 * r, TV + nx + 12 * i);
+        QV[e] = v + re[t];
+      }
+    }
+    __syncthreads();
+    PROF_ADD(3);
+    // Twisted block solve (pdipm_srbd.hpp FastCtx::solve), w / v in registers.
+    if (lane < 32) {
+      const int g = lane >> 4, l16 = lane & 15;
+      const int r = l16 < 12 ? l16 : 11;
+      const bool own = l16 < 12;
+      const int pr = g ? perm12(r) : r;
+      const int cnt = g ? nb : nf;
+      const double* cc = at(Lo::Cc) + 24 * g;
+      double Crow[12], Ccol[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        Crow[j] = cel(cc, r, j);
+        Ccol[j] = cel(cc, j, r);
+      }
+      double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
+#pragma unroll
+      for (int k = 0; k <= T; ++k) wv[k] = 0.0;
+#pragma unroll 1
+      for (int t = 0; t <= T; ++t) {
+        const bool mstep = (t == T);
+        const int i = mstep ? mid : (g ? N - 1 - t : t);
+        const bool act = mstep ? true : (t < cnt);
+        const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+        double cw = 0.0;
+        if (act && prev) {
+          double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            c0 += Crow[j] * bc16(w, j);
+            c1 += Crow[j + 4] * bc16(w, j + 4);
+            c2 += Crow[j + 8] * bc16(w, j + 8);
+          }
+          cw = (c0 + c1) + c2;
+        }
+        double mv = 0.0;
+        if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
+        if (act && !(mstep && g == 1)) {
+          const double* Di = DV + 78 * i;
+          double Dr[12];
+#pragma unroll
+          for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12c(k) : k)];
+          const double q = (QV[12 * i + pr] - cw) - mv;
+          double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            a0 += Dr[k] * bc16(q, k);
+            a1 += Dr[k + 4] * bc16(q, k + 4);
+            a2 += Dr[k + 8] * bc16(q, k + 8);
+          }
+          w = (a0 + a1) + a2;
+#pragma unroll
+          for (int k = 0; k <= T; ++k) wv[k] = (k == t) ? w : wv[k];
+        }
+      }
+      // outward substitution from y_mid (group 0's last w; group 1 fetches row pi(r) of it)
+      const double ym = __shfl(w, perm12(r), 64);
+      if (own && g == 0) QV[12 * mid + r] = w;
+      double y = g ? ym : w;
+#pragma unroll 1
+      for (int t = 0; t < T; ++t) {
+        const int i = g ? mid + 1 + t : mid - 1 - t;
+        if (t < cnt) {
+          const int te = g ? N - 2 - mid - t : mid - 1 - t;  // elimination step of stage i
+          double wprev = 0.0;
+#pragma unroll
+          for (int k = 0; k <= T; ++k) wprev = (k == te) ? wv[k] : wprev;
+          const double* Di = DV + 78 * i;
+          double Dr[12];
+#pragma unroll
+          for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12c(k) : k)];
+          double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // Cg^T y_prev
+            s0 += Ccol[j] * bc16(y, j);
+            s1 += Ccol[j + 4] * bc16(y, j + 4);
+            s2 += Ccol[j + 8] * bc16(y, j + 8);
+          }
+          const double sc = (s0 + s1) + s2;
+          double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            a0 += Dr[k] * bc16(sc, k);
+            a1 += Dr[k + 4] * bc16(sc, k + 4);
+            a2 += Dr[k + 8] * bc16(sc, k + 8);
+          }
+          y = wprev - ((a0 + a1) + a2);
+          if (own) QV[12 * i + pr] = y;
+        }
+      }
+    }
+    __syncthreads();
+    PROF_ADD(4);
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
+      const int c = lane + 64 * t;
+      if (c < nx) {
+        const int k = c / 12 + 1, j = c % 12;
+        double aty = Pd[j] * QV[12 * (k - 1) + j];
+        if (k < N) aty += mcol(Mc, j, QV + 12 * k);
+        TV[c] = TV[c] - aty * IX[j];
+      }
+    }
+    if (lane < 3 * N) {
+      const bool foot = lane < 2 * N;
+      const int i = foot ? (lane >> 1) : lane - 2 * N;
+      const int b = nx + 12 * i;
+      const double* yi = QV + 12 * i;
+      if (foot) {
+        const int f = lane & 1;
+        double av[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) av[a] = dcol12(Nd, foot_colj(f, a), yi);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
+          TV[b + foot_colj(f, a)] -= t;
+        }
+      } else {
+        const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
+        const double a6 = dcol12(Nd, 6, yi), a9 = dcol12(Nd, 9, yi);
+        const double a8 = dcol12(Nd, 8, yi), a11 = dcol12(Nd, 11, yi);
+        TV[b + 6] -= SG[0] * a6;
+        TV[b + 9] -= SG[2] * a9;
+        TV[b + 8] -= SG[1] * a8;
+        TV[b + 11] -= SG[3] * a11;
+        const double rho6 = -RXu[12 * i + 6] - a6, rho9 = -RXu[12 * i + 9] - a9;
+        DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
+        DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // dz, ds (owner regs)
+      const int q = lane + 64 * t;
+      if (q < m) {
+        const int i = q / 16, k = q % 16;
+        const double gd = grow4(Gf, k, TV + nx + 12 * i);
+        dz[t] = VV[q] + di[t] * wd[t] * gd;
+        ds[t] = -rs[t] - gd + kDelta * dz[t];
+      }
+    }
+    PROF_ADD(3);
+  }
+
+  __device__ double step_length(const double (&v)[SI], const double (&dv)[SI]) const {
+    const int lane = fresh_lane();
+    double mn = INFINITY;
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + 64 * t;
+      if (q < m) {
+        const bool c = dv[t] < 0.0;
+        const double a = -v[t] / dv[t];
+        mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
+      }
+    }
+    mn = wave_min(mn);
+    return fmax(fmin(1.0, 0.99 * mn), 1e-12);
+  }
+};
+
+template <int N>
+__global__ __launch_bounds__(64, 2) void pdipm_srbd_reg_kernel(SolverArgs args) {
+  using Lo = RegLayout<N>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int env = blockIdx.x;
+  if (env >= args.batch) return;
+  const int lane = threadIdx.x;
+  constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
+  const int nA = nnz_A(N), nG = 28 * N;
+  RegCtx<N> C;
+  C.L = smem;
+  C.lane = lane;
+  const double* Hg = solver_in(args, 0) + (size_t)env * nz;
+  const double* Gg = solver_in(args, 1) + (size_t)env * nG;
+  const double* Ag = solver_in(args, 2) + (size_t)env * nA;
+  C.fg = solver_in(args, 3) + (size_t)env * nz;
+  C.hg = solver_in(args, 4) + (size_t)env * m;
+  C.bg = solver_in(args, 5) + (size_t)env * p;
+  double *Mc = smem + Lo::Mc, *Cc = smem + Lo::Cc, *Nd = smem + Lo::Nd, *Gf = smem + Lo::Gf,
+         *K0 = smem + Lo::K0, *K1 = smem + Lo::K1, *Pd = smem + Lo::Pd, *IX = smem + Lo::IX,
+         *Hu = smem + Lo::Hu, *SG = smem + Lo::SG;
+  double* Md = smem + Lo::TV;  // dense M while the constants are built (TV is free until solve)
+
+  // ---- compact load (stage 0/1 slices) ----
+  for (int e = lane; e < 144; e += 64) {
+    const int r = e / 12, j = e % 12;
+    const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
+    Md[e] = (N >= 2 && om >= 0) ? Ag[a_xblock(1) + om] : 0.0;
+    Nd[e] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
+  }
+  Gf[lane] = 0.0;  // 64 entries
+  if (lane < 12) {
+    Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
+    Hu[lane] = Hg[nx + lane];
+    Hu[12 + lane] = Hg[lane];
+  }
+  __syncthreads();
+  if (lane < 28) Gf[4 * c_tab.grow[lane] + foot_pos(c_tab.gcol[lane])] = Gg[lane];
+  // ---- stage-invariance check (bitwise), as pdipm_srbd_kernel ----
+  bool bad = false;
+  for (int e = lane; e < nA; e += 64) {
+    double ref;
+    if (e < 36 * (N - 1)) {
+      const int loc = e % 36;
+      int j = 11;
+      while (c_tab.cpx[j] > loc) --j;
+      const int t = loc - c_tab.cpx[j];
+      ref = (t == 0) ? Pd[j] : Md[c_tab.sx[j][t - 1] * 12 + j];
+    } else if (e < a_ubase(N)) {
+      ref = Pd[e - 36 * (N - 1)];
+    } else {
+      const int loc = (e - a_ubase(N)) % 86;
+      int j = 11;
+      while (c_tab.cpu[j] > loc) --j;
+      const int t = loc - c_tab.cpu[j];
+      ref = (t < c_tab.su_n[j]) ? Nd[c_tab.su[j][t] * 12 + j] : Ag[a_ubase(N) + loc];
+    }
+    bad |= !(Ag[e] == ref);
+  }
+  for (int e = lane; e < nG; e += 64) bad |= !(Gg[e] == Gg[e % 28]);
+  for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
+  if (__any(bad)) {
+    if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
+    return;
+  }
+  // ---- per-QP constants ----
+  if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
+  if (lane == 0) {
+    const double e6 = Ag[a_ubase(N) + c_tab.e6], e9 = Ag[a_ubase(N) + c_tab.e9];
+    const double p6 = Hu[6] + kBeta, p9 = Hu[9] + kBeta;
+    SG[0] = kDelta / (p6 * kDelta + e6 * e6);
+    SG[1] = 1.0 / (Hu[8] + kBeta);
+    SG[2] = kDelta / (p9 * kDelta + e9 * e9);
+    SG[3] = 1.0 / (Hu[11] + kBeta);
+    SG[4] = p6;
+    SG[5] = p9;
+    SG[6] = e6;
+    SG[7] = e9;
+  }
+  __syncthreads();
+  if (lane < 24) {  // compact M and C (C = M diag(P / phi_x)); group 1's block is pi C^T pi^T
+    int r, j;
+    if (lane < 12) { r = lane; j = lane; }
+    else if (lane < 21) { r = (lane - 12) / 3; j = 6 + (lane - 12) % 3; }
+    else { r = lane - 21 + 3; j = r + 6; }
+    const double mv = Md[r * 12 + j];
+    Mc[lane] = mv;
+    const double cv = mv * (Pd[j] * IX[j]);
+    Cc[lane] = cv;
+    // pi C^T pi^T: diag c <- C[pi c][pi c]; a-part (c, 6+k) <- C[k][c+6]; b-part unchanged
+    int l1;
+    if (lane < 12) l1 = perm12c(lane);
+    else if (lane < 21) l1 = 12 + 3 * (j - 6) + r;  // entry (r, 6 + k) lands at (k, 6 + r)
+    else l1 = lane;
+    Cc[24 + l1] = cv;
+  }
+  for (int e = lane; e < 78; e += 64) {
+    int r, c;
+    tri_rc(e, r, c);
+    double k0 = (r == c) ? Pd[r] * Pd[r] * IX[r] + kDelta : 0.0;
+    k0 += Nd[r * 12 + 6] * Nd[c * 12 + 6] * SG[0] + Nd[r * 12 + 8] * Nd[c * 12 + 8] * SG[1] +
+          Nd[r * 12 + 9] * Nd[c * 12 + 9] * SG[2] + Nd[r * 12 + 11] * Nd[c * 12 + 11] * SG[3];
+    double k1 = k0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) k1 += Md[r * 12 + j] * Md[c * 12 + j] * IX[j];
+    K0[e] = k0;
+    K1[e] = k1;
+  }
+  // ---- iterate ----
+  double *X = smem + Lo::X, *Z = smem + Lo::Z, *Y = smem + Lo::Y;
+  if (args.init_mode == 0) {
+    const double* xg = solver_in(args, 6) + (size_t)env * nz;
+    const double* sg = solver_in(args, 7) + (size_t)env * m;
+    const double* zg = solver_in(args, 8) + (size_t)env * m;
+    const double* yg = solver_in(args, 9) + (size_t)env * p;
+    for (int e = lane; e < nz; e += 64) X[e] = xg[e];
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + 64 * t;
+      if (q < m) {
+        C.s[t] = sg[q];
+        C.z[t] = zg[q];
+        Z[q] = C.z[t];
+      }
+    }
+    for (int e = lane; e < p; e += 64) Y[e] = yg[e];
+  } else {
+    for (int e = lane; e < nz; e += 64) X[e] = 0.0;
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + 64 * t;
+      if (q < m) {
+        C.s[t] = fmax(C.hg[q] - 0.0, 1.0);
+        C.z[t] = 1.0;
+        Z[q] = 1.0;
+      }
+    }
+    for (int e = lane; e < p; e += 64) Y[e] = args.y0;
+  }
+  __syncthreads();
+
+  double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
+  const double* TV = smem + Lo::TV;
+  const double* QV = smem + Lo::QV;
+  const double* DYm = smem + Lo::DYm;
+  const double* RXu = smem + Lo::RXu;
+  PROF_MARK_CTX(C);
+  for (int it = 0; it < args.n_iter; ++it) {
+    const double mu = C.residuals();
+    PROF_ADD_CTX(C, 0);
+    C.factor();
+    C.solve(0, 0.0);
+    const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
+    double sza = 0.0;
+    int ul = C.fresh_lane();
+#pragma unroll
+    for (int t = 0; t < SI; ++t)
+      if (ul + 64 * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
+    const double mu_aff = wave_sum(sza) / m;
+    const double ratio = mu_aff / mu;
+    const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
+    __syncthreads();
+    PROF_ADD_CTX(C, 5);
+    C.solve(1, sigma * mu * 1.0);
+    const double apc = C.step_length(C.s, C.ds), adc = C.step_length(C.z, C.dz);
+    __syncthreads();
+    double szn = 0.0;
+    ul = C.fresh_lane();
+    for (int e = ul; e < nz; e += 64) X[e] = X[e] + apc * TV[e];
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = ul + 64 * t;
+      if (q < m) {
+        const double sn = fmax(C.s[t] + apc * C.ds[t], 1e-8);
+        const double zn = fmax(fmax(C.z[t] + adc * C.dz[t], 1e-8), 1e-8);
+        C.s[t] = sn;
+        C.z[t] = zn;
+        Z[q] = zn;
+        szn += sn * zn;
+      }
+    }
+    for (int e = ul; e < p; e += 64) Y[e] = Y[e] + adc * (e < nx ? QV[e] : DYm[e - nx]);
+    mu_new = wave_sum(szn) / m;
+    if (it == args.n_iter - 1) {
+      double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+      for (int t = 0; t < Lo::SX; ++t)
+        if (ul + 64 * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + 64 * t] * RXu[ul + 64 * t];
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (ul + 64 * t < m) b += C.rs[t] * C.rs[t];
+#pragma unroll
+      for (int t = 0; t < Lo::SE; ++t)
+        if (ul + 64 * t < p) c += C.re[t] * C.re[t];
+      res0 = sqrt(wave_sum(a));
+      res1 = sqrt(wave_sum(b));
+      res2 = sqrt(wave_sum(c));
+    }
+    __syncthreads();
+    PROF_ADD_CTX(C, 5);
+  }
+  PROF_FLUSH(C);
+  double* xo = solver_out(args, 0) + (size_t)env * nz;
+  double* so = solver_out(args, 1) + (size_t)env * m;
+  double* zo = solver_out(args, 2) + (size_t)env * m;
+  double* yo = solver_out(args, 3) + (size_t)env * p;
+  double* ro = solver_out(args, 4) + (size_t)env * 4;
+  double* mo = solver_out(args, 5) + (size_t)env;
+  for (int e = lane; e < nz; e += 64) xo[e] = X[e];
+#pragma unroll
+  for (int t = 0; t < SI; ++t) {
+    const int q = lane + 64 * t;
+    if (q < m) {
+      so[q] = C.s[t];
+      zo[q] = C.z[t];
+    }
+  }
+  for (int e = lane; e < p; e += 64) yo[e] = Y[e];
+  if (lane == 0) {
+    ro[0] = res0;
+    ro[1] = res1;
+    ro[2] = res2;
+    ro[3] = mu_new;
+    mo[0] = mu_new;
+  }
+}
+
+}  // namespace srbd

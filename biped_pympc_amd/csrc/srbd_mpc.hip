@@ -12,6 +12,7 @@
 #include "../../include/srbd_mpc.h"
 #include "pdipm.hpp"
 #include "pdipm_srbd.hpp"
+#include "pdipm_srbd_reg.hpp"
 #include "qp_former.hpp"
 
 namespace {
@@ -33,8 +34,11 @@ bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 
 size_t solver_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::SolverLayout(N).total; }
 size_t fast_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::FastLayout(N).total; }
+constexpr size_t kRegLds10 = sizeof(double) * (size_t)srbd::RegLayout<10>::total;
+static_assert(kRegLds10 <= 20 * 1024, "N=10 register kernel must fit 8 QPs per CU");
 
-// 0 = auto (fast stage-invariant kernel, general kernel for flagged QPs); 1 = general kernel only
+// 0 = auto (stage-invariant kernels -- register-resident for N = 10, LDS-resident otherwise -- and
+// the general kernel for flagged QPs); 1 = general kernel only; 2 = LDS-resident fast kernel
 int g_solver_path = 0;
 
 int ensure_lds_attr(const void* fn, size_t bytes, size_t* configured) {
@@ -57,10 +61,16 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
-  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0;
+  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0, cfg_reg10 = 0;
   srbd::SolverArgs a = a0;
   a.only_flagged = 0;
-  if (g_solver_path == 0) {
+  if (g_solver_path == 0 && a.N == 10) {
+    if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, &cfg_reg10)) return rc;
+    hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
+    a.only_flagged = 1;
+  } else if (g_solver_path == 0 || g_solver_path == 2) {
     const size_t lds = fast_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
     // horizon-specialised instantiations for the common horizons, runtime-N otherwise
@@ -131,7 +141,8 @@ int srbd_debug_phase_cycles(unsigned long long* out16) {
 #endif
 
 int srbd_set_solver_path(int path) {
-  if (path != 0 && path != 1) return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto) or 1 (general)");
+  if (path < 0 || path > 2)
+    return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto), 1 (general) or 2 (LDS-resident fast)");
   g_solver_path = path;
   return 0;
 }

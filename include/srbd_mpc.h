@@ -76,8 +76,10 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 /* LDS bytes one solver workgroup (one QP) uses at this horizon (0 if unsupported). */
 size_t srbd_solver_lds_bytes(int horizon);
 
-/* Solver kernel selection: 0 = auto (default): the fast kernel for stage-invariant QPs (every QP
- * qp_former emits), the general kernel for any other QP in the batch; 1 = general kernel only.
+/* Solver kernel selection: 0 = auto (default): a stage-invariant kernel for stage-invariant QPs
+ * (every QP qp_former emits; register-resident at N = 10, LDS-resident otherwise), the general
+ * kernel for any other QP in the batch; 1 = general kernel only; 2 = LDS-resident stage-invariant
+ * kernel at every horizon (plus the general fallback).
  * Results agree to round-off (tests/test_gpu_parity.py). Process-wide. */
 int srbd_set_solver_path(int path);
 
