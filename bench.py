@@ -68,14 +68,21 @@ def event_time_ms(fn, reps: int) -> float:
     return e0.elapsed_time(e1) / reps
 
 
+def solver_kernel_name(N: int) -> str:
+    """The stage-invariant solver kernel launch_solver picks for horizon N (srbd_mpc.hip)."""
+    return f"pdipm_srbd_reg_kernel<{N}>" if N == 10 else f"pdipm_srbd_kernel<{N if N == 20 else 0}>"
+
+
 def load_pmc(N: int, B: int, K: int):
-    """HBM bytes per pdipm launch from the committed rocprofv3 --pmc summary, if one matches."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    """HBM bytes per solver launch from the committed rocprofv3 --pmc summary of this kernel."""
+    name = solver_kernel_name(N)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json"))):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if d.get("horizon") == N and d.get("batch") == B and d.get("iters") == K:
+        if (d.get("horizon") == N and d.get("batch") == B and d.get("iters") == K
+                and name in (d.get("kernel") or "")):
             return d.get("pdipm_hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
@@ -147,7 +154,7 @@ def main():
         achieved = flops / (ms_pdipm * 1e-3) / 1e12
         traffic, traffic_src = load_pmc(N, B, K)
         roofline = {
-            "bound": "mfma", "kernel": f"pdipm_srbd_kernel<{N if N in (10, 20) else 0}>", "achieved": round(achieved, 4),
+            "bound": "mfma", "kernel": solver_kernel_name(N), "achieved": round(achieved, 4),
             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
             "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_pdipm, 4),

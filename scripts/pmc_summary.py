@@ -40,9 +40,11 @@ def main():
         kernels[k] = {"dispatches": nf.get(k, 0), "fetch_size_raw_bytes": f_raw,
                       "fetch_bytes_corrected": 2.0 * f_raw, "write_bytes": w,
                       "hbm_bytes": 2.0 * f_raw + w}
-    pd = [v for k, v in kernels.items() if "pdipm_srbd_kernel" in k]
+    # the solver kernel = the stage-invariant one that moved the most bytes
+    pd = sorted((v["hbm_bytes"], k) for k, v in kernels.items() if "pdipm_srbd" in k)
     out = {"horizon": a.horizon, "batch": a.batch, "iters": a.iters,
-           "pdipm_hbm_bytes_per_launch": pd[0]["hbm_bytes"] if pd else None,
+           "kernel": pd[-1][1] if pd else None,
+           "pdipm_hbm_bytes_per_launch": pd[-1][0] if pd else None,
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "kernels": kernels}
     with open(a.out, "w") as fh:
