@@ -70,7 +70,7 @@ def event_time_ms(fn, reps: int) -> float:
 
 def solver_kernel_name(N: int) -> str:
     """The stage-invariant solver kernel launch_solver picks for horizon N (srbd_mpc.hip)."""
-    return f"pdipm_srbd_reg_kernel<{N}>" if N == 10 else f"pdipm_srbd_kernel<{N if N == 20 else 0}>"
+    return f"pdipm_srbd_reg_kernel<{N}>" if N in (10, 20) else "pdipm_srbd_kernel<0>"
 
 
 def load_pmc(N: int, B: int, K: int):

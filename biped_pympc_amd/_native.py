@@ -80,7 +80,7 @@ def check(rc: int, what: str) -> None:
 
 class solver_path:
     """Context manager selecting the solver kernels: "auto" (stage-invariant kernels -- the
-    register-resident one at N = 10 -- plus the general fallback), "general" (general kernel only)
+    register-resident one at N = 10 and 20 -- plus the general fallback), "general" (general kernel only)
     or "lds" (the LDS-resident stage-invariant kernel at every horizon). Process-wide; for
     tests/benchmarks."""
 

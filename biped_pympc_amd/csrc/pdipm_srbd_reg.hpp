@@ -569,7 +569,8 @@ struct RegCtx {
 };
 
 template <int N>
-__global__ __launch_bounds__(64, 2) void pdipm_srbd_reg_kernel(SolverArgs args) {
+// N <= 10: 2 waves per SIMD (<= 256 registers); longer horizons: LDS allows 1 wave per SIMD anyway
+__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(SolverArgs args) {
   using Lo = RegLayout<N>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = blockIdx.x;

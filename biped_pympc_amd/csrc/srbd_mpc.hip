@@ -35,9 +35,10 @@ bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 size_t solver_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::SolverLayout(N).total; }
 size_t fast_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::FastLayout(N).total; }
 constexpr size_t kRegLds10 = sizeof(double) * (size_t)srbd::RegLayout<10>::total;
+constexpr size_t kRegLds20 = sizeof(double) * (size_t)srbd::RegLayout<20>::total;
 static_assert(kRegLds10 <= 20 * 1024, "N=10 register kernel must fit 8 QPs per CU");
 
-// 0 = auto (stage-invariant kernels -- register-resident for N = 10, LDS-resident otherwise -- and
+// 0 = auto (stage-invariant kernels -- register-resident for N = 10 and 20, LDS-resident otherwise -- and
 // the general kernel for flagged QPs); 1 = general kernel only; 2 = LDS-resident fast kernel
 int g_solver_path = 0;
 
@@ -61,12 +62,17 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
-  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0, cfg_reg10 = 0;
+  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0, cfg_reg10 = 0, cfg_reg20 = 0;
   srbd::SolverArgs a = a0;
   a.only_flagged = 0;
-  if (g_solver_path == 0 && a.N == 10) {
-    if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, &cfg_reg10)) return rc;
-    hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
+  if (g_solver_path == 0 && (a.N == 10 || a.N == 20)) {
+    if (a.N == 10) {
+      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, &cfg_reg10)) return rc;
+      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
+    } else {
+      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, &cfg_reg20)) return rc;
+      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(64), kRegLds20, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
     a.only_flagged = 1;

@@ -77,7 +77,7 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 size_t srbd_solver_lds_bytes(int horizon);
 
 /* Solver kernel selection: 0 = auto (default): a stage-invariant kernel for stage-invariant QPs
- * (every QP qp_former emits; register-resident at N = 10, LDS-resident otherwise), the general
+ * (every QP qp_former emits; register-resident at N = 10 and 20, LDS-resident otherwise), the general
  * kernel for any other QP in the batch; 1 = general kernel only; 2 = LDS-resident stage-invariant
  * kernel at every horizon (plus the general fallback).
  * Results agree to round-off (tests/test_gpu_parity.py). Process-wide. */
