@@ -40,6 +40,38 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
+// Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r in lane r of a 16-lane
+// DPP row; lanes 12..15 shadow row 11), by Gauss-Jordan pivoting on the diagonal. Unlike sweep12 the
+// pivot row is not rescaled in place: every lane keeps its row unscaled together with a scale
+// factor (1/pivot once the row has been the pivot) that is applied once at the end, so each pivot
+// costs 11 FMAs per lane (no per-element select or multiply for the pivot lane).
+//   pivot k (pk = row k, broadcast with v_mov_b64_dpp row_newbcast, id = 1/pk[k]):
+//     lane r != k: a_rj <- a_rj - a_rk id pk_j  (j != k),  a_rk <- a_rk id
+//     lane k     : row unchanged except a_kk <- -1, scale <- id
+// On exit Dr[j] = (A^-1)_rj.
+__device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (&Dr)[12]) {
+  double sc = 1.0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    double pk[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) pk[j] = bc16(Sr[j], k);
+    const double id = rcp_nr(pk[k]);
+    const bool piv = (r == k);
+    const double ark = Sr[k];
+    const double coef = piv ? 0.0 : -ark * id;
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+      if (j != k) Sr[j] = fma(coef, pk[j], Sr[j]);
+    Sr[k] = piv ? -1.0 : ark * id;
+    sc = piv ? id : sc;
+  }
+  // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
+  const double nsc = -sc;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) Dr[j] = Sr[j] * nsc;
+}
+
 // element (c, b) of a compact M / C block (c or b runtime)
 __device__ __forceinline__ double cel(const double* cc, int c, int b) {
   if (b == c) return cc[c];
@@ -316,9 +348,7 @@ struct RegCtx {
           }
         }
         if (act && !(mstep && g == 1)) {
-          sweep12(Sr, r);
-#pragma unroll
-          for (int c = 0; c < 12; ++c) Dr[c] = -Sr[c];
+          inverse_rows12(Sr, r, Dr);
           if (own) {
             double* Di = DV + 78 * i;
 #pragma unroll
