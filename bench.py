@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 from biped_pympc_amd import solver  # noqa: E402
 from biped_pympc_amd.layout import Dims  # noqa: E402
+from biped_pympc_amd.sharding import ShardedMPC  # noqa: E402
 from biped_pympc_amd.utils.synthetic import make_workload  # noqa: E402
 
 # Structural work per solve, frozen from scripts/algorithmic_work.py (SURVEY.md 8d convention:
@@ -103,17 +104,13 @@ def main():
     N, K, B = a.horizon, a.iters, a.batch_per_gpu
     d = Dims(N)
 
+    # each rank's shard of the global synthetic batch (world x B robots) is generated locally
     wl = make_workload(B, N, seed=1000 + rank, random_gait=a.random_gait)
     inputs = [torch.from_numpy(x).to(dev) for x in wl.inputs]
-    bufs = solver.MPCSolveBuffers.allocate(N, B, dev)
-    u0_all = torch.empty((world * B, 12), dtype=torch.float64, device=dev) if world > 1 else None
+    sh = ShardedMPC(N, K, world * B, device=dev, y0=1.0)
 
     def step():
-        out = solver.mpc_solve(inputs, N, K, y0=1.0, buffers=bufs)
-        if dist is not None:
-            u0 = out[0][:, 12 * N:12 * N + 12].contiguous()
-            dist.all_gather_into_tensor(u0_all, u0)
-        return out
+        return sh.step(inputs)  # former + PDIPM on this shard, then the u0 gather (RCCL) if world > 1
 
     for _ in range(a.warmup):
         step()
@@ -136,6 +133,7 @@ def main():
     value = world * B * a.steps / elapsed
 
     # per-kernel timing (HIP events on the launch stream), former output already in the workspace
+    bufs = sh.buffers
     qp = bufs.qp_views()
     sol_qp = [qp[0], qp[4], qp[2], qp[1], qp[5], qp[3]]  # H, G, A, f, h(=d), b
     pd_out = solver._alloc_solver_outputs(B, N, dev)
@@ -144,8 +142,8 @@ def main():
                              a.kernel_reps)
     ms_gather = None
     if dist is not None:
-        u0 = bufs.outputs[0][:, 12 * N:12 * N + 12].contiguous()
-        ms_gather = event_time_ms(lambda: dist.all_gather_into_tensor(u0_all, u0), a.kernel_reps)
+        u0 = bufs.outputs[0][:, 12 * N:12 * N + 12]
+        ms_gather = event_time_ms(lambda: sh.gather_u0(u0), a.kernel_reps)
 
     w = WORK.get(N)
     roofline = None
@@ -186,9 +184,9 @@ def main():
                "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs) on the first "
                           f"{sample} envs of the same workload, {solves // sample} passes, "
                           f"{t_cpu:.1f} s, N={N}, {K} iterations")}
-        out = step()
+        step()
         torch.cuda.synchronize()
-        x = out[0][:sample].cpu().numpy()
+        x = sh.x_local[:sample].cpu().numpy()
         ug, ur = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
         du = np.abs(ug - ur)
         parity = {"max_abs_du": float(du.max()),
