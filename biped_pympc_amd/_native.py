@@ -63,8 +63,27 @@ def lib() -> ctypes.CDLL:
     L.srbd_pattern_ccs.restype = ctypes.c_int
     L.srbd_pattern_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_int)]
+    L.srbd_prepare_inputs.restype = ctypes.c_int
+    L.srbd_prepare_inputs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(MPCPrep), P, ctypes.c_void_p]
+    L.srbd_u0_wrench.restype = ctypes.c_int
+    L.srbd_u0_wrench.argtypes = [ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
+    L.srbd_dense_scatter.restype = ctypes.c_int
+    L.srbd_dense_scatter.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp,
+                                     ctypes.c_void_p]
     _lib = L
     return L
+
+
+class MPCPrep(ctypes.Structure):
+    """ctypes mirror of ``srbd_mpc_prep`` (include/srbd_mpc.h); device pointers as void*."""
+    _fields_ = [(n, _c_dp) for n in (
+        "root_euler", "root_position", "root_angular_velocity_w", "root_velocity_w", "rotation_body",
+        "foot_position", "desired_velocity_b", "desired_angular_velocity_b", "desired_height",
+        "world_position_desired", "yaw_desired", "first_run", "gait_phase", "ssp_durations",
+        "dsp_durations", "contact_table", "dt_mpc", "residual_lin_accel", "residual_ang_accel")] + [
+        ("I_body", ctypes.c_float * 9), ("mass", ctypes.c_double), ("mu", ctypes.c_double),
+        ("Q", ctypes.c_float * 13), ("q_len", ctypes.c_int), ("R", ctypes.c_float * 12),
+        ("step_dt", ctypes.c_float), ("literal_layout", ctypes.c_int)]
 
 
 def ptr_array(ptrs) -> ctypes.Array:

@@ -1,0 +1,276 @@
+"""Batched convex-MPC controller over the HIP path -- the caller side of the hot path.
+
+Mirrors the reference controller API so a user of ``MPCControllerCusadi`` can switch:
+  * ``MPCConf`` (reference ``biped_pympc/configuration/configuration.py:23-70``),
+  * ``StateEStimatorData`` / ``DesiredStateData`` (``biped_pympc/core/data/robot_data.py:9-60``),
+  * ``BaseMPCController`` setters and knot-point state (``convex_mpc/base_controller.py:11-266``),
+  * ``MPCControllerHIP.run() -> (foot_wrench (B,2,6) float32, cost (B,))`` with the semantics of
+    ``MPCControllerCusadi.run`` (``convex_mpc/mpc_controller_cusadi.py:43-205``).
+The whole step runs as four kernels on the caller's current HIP stream with no host
+synchronisation: ``srbd_prepare_inputs`` (knot points, initial state, reference trajectory,
+contact schedule, I_world -- the ~40 small FP32 torch ops of the reference), ``qp_former``, the
+PDIPM (cold start, ``cfg.pdipm_iterations`` Newton iterations in one launch; the reference runs
+4 calls x 5 iterations with host round trips) and ``srbd_u0_wrench``. Nothing of the step is
+computed in PyTorch; it only owns the buffers.
+
+``literal_layout=True`` (default) reproduces the reference GPU caller's flattening quirks
+(row-major R_body read column-major, row-major contact table read column-major, a 13-wide Q read
+with stride 12: SURVEY.md Appendix B.1-B.3) so results match the reference; ``False`` lays the
+inputs out the way the QP model means them.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Tuple, Union
+
+import torch
+
+from biped_pympc_amd import _native, solver
+from biped_pympc_amd.layout import Dims
+
+# robot constants (reference core/robot/hector.py:33-38, core/robot/t1.py:70-75)
+ROBOTS = {
+    "HECTOR": {"mass": 13.856, "mu": 1.0, "I_body": ((0.5413, 0.0, 0.0), (0.0, 0.5200, 0.0), (0.0, 0.0, 0.0691))},
+    "T1": {"mass": 40.0, "mu": 1.0, "I_body": ((0.5413, 0.0, 0.0), (0.0, 0.5200, 0.0), (0.0, 0.0, 0.0691))},
+}
+
+
+@dataclass
+class MPCConf:
+    """MPC configuration (configuration.py:23-57), plus the HIP path's own knobs."""
+    dt: float = 0.001
+    dt_mpc: float = 0.025
+    horizon_length: int = 10
+    decimation: int = 10
+    Q: torch.Tensor = field(default_factory=lambda: torch.tensor(
+        [150, 150, 250, 100, 100, 250, 1, 1, 5, 10, 10, 1, 1], dtype=torch.float32))
+    R: torch.Tensor = field(default_factory=lambda: torch.tensor(
+        [1e-5, 1e-5, 1e-5, 1e-5, 1e-5, 1e-5, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4], dtype=torch.float32))
+    print_solve_time: bool = False
+    solver: str = "hip"
+    robot: str = "HECTOR"
+    pdipm_iterations: int = 20  # the reference GPU caller: 4 calls x 5 iterations (:28, :144)
+    y0: float = 1.0             # dual init of the GPU caller (:141)
+    literal_layout: bool = True
+
+
+@dataclass
+class StateEStimatorData:
+    """Robot state estimate (robot_data.py:9-26), float32, world frame unless noted."""
+    num_legs: int = 2
+    batch_size: int = 1
+    device: Union[torch.device, str] = "cpu"
+
+    def __post_init__(self):
+        B, dev = self.batch_size, self.device
+        self.root_position = torch.zeros((B, 3), device=dev)
+        self.root_quat = torch.zeros((B, 4), device=dev)
+        self.root_quat[:, 0] = 1.0
+        self.root_euler = torch.zeros((B, 3), device=dev)
+        self.rotation_body = torch.eye(3, device=dev).unsqueeze(0).repeat(B, 1, 1)
+        self.root_velocity_w = torch.zeros((B, 3), device=dev)
+        self.root_angular_velocity_w = torch.zeros((B, 3), device=dev)
+        self.foot_position = torch.zeros((B, self.num_legs, 3), device=dev)
+        self.root_velocity_b = torch.zeros((B, 3), device=dev)
+        self.root_angular_velocity_b = torch.zeros((B, 3), device=dev)
+
+
+@dataclass
+class DesiredStateData:
+    """Commanded motion in the body frame (robot_data.py:41-60)."""
+    batch_size: int = 1
+    device: Union[torch.device, str] = "cpu"
+
+    def __post_init__(self):
+        B, dev = self.batch_size, self.device
+        self.desired_velocity_b = torch.zeros((B, 3), device=dev)
+        self.desired_angular_velocity_b = torch.zeros((B, 3), device=dev)
+        self.desired_height = 0.55 * torch.ones(B, device=dev)
+        self.desired_position = torch.zeros((B, 3), device=dev)
+        self.desired_angle = torch.zeros((B, 3), device=dev)
+
+    def set_command(self, desired_lin_velocity, desired_ang_velocity, desired_height) -> None:
+        self.desired_velocity_b[:, :2] = desired_lin_velocity
+        self.desired_angular_velocity_b[:, 2] = desired_ang_velocity
+        self.desired_height[:] = desired_height
+
+
+def _f32(t: torch.Tensor, device) -> torch.Tensor:
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+class BaseMPCController:
+    """Knot-point state, setters and buffers shared by MPC controllers (base_controller.py:11-266)."""
+
+    def __init__(self, num_envs: int, device: Union[torch.device, str], num_legs: int, cfg: MPCConf):
+        self.cfg = cfg
+        self.num_envs = num_envs
+        self.num_legs = num_legs
+        self.device = torch.device(device)
+        self.horizon_length = cfg.horizon_length
+        self.dt = cfg.dt
+        self.dt_mpc = cfg.dt_mpc * torch.ones(num_envs, device=self.device)
+        self.state_estimate_data: StateEStimatorData | None = None
+        self.desired_state_data: DesiredStateData | None = None
+        self.leg_controller_data = None
+        self.first_run = torch.ones(num_envs, device=self.device, dtype=torch.bool)
+        robot = ROBOTS[cfg.robot]
+        self.mass, self.mu = robot["mass"], robot["mu"]
+        self.I_body = torch.tensor(robot["I_body"], dtype=torch.float32)
+        self.init_buffer()
+        self.init_solver()
+
+    def init_buffer(self) -> None:
+        B, N, dev = self.num_envs, self.horizon_length, self.device
+        self.contact_table = torch.ones((B, N, 2), device=dev)
+        self.world_position_desired = torch.zeros((B, 3), device=dev)
+        self.yaw_desired = torch.zeros(B, device=dev)
+        self.residual_lin_accel = torch.zeros((B, 3), device=dev)
+        self.residual_ang_accel = torch.zeros((B, 3), device=dev)
+        self.Q = self.cfg.Q
+        self.R = self.cfg.R
+        self._gait = None  # (phase (B,), ssp (B,2) int32, dsp (B,2) int32) for the device-side schedule
+
+    def init_solver(self) -> None:
+        raise NotImplementedError
+
+    # ---- setters (base_controller.py:98-142) ----
+    def set_state_estimate_data(self, state_estimate_data: StateEStimatorData) -> None:
+        self.state_estimate_data = state_estimate_data
+
+    def set_desired_state_data(self, desired_state_data: DesiredStateData) -> None:
+        self.desired_state_data = desired_state_data
+
+    def set_leg_controller_data(self, leg_controller_data) -> None:
+        self.leg_controller_data = leg_controller_data
+
+    def set_contact_table(self, contact_table: torch.Tensor) -> None:
+        """Explicit (B, N, 2) contact schedule (what GaitGenerator.mpc_gait returns)."""
+        self.contact_table = _f32(contact_table, self.device)
+        self._gait = None
+
+    def set_gait(self, gait_phase: torch.Tensor, ssp_durations: torch.Tensor, dsp_durations: torch.Tensor) -> None:
+        """Device-side contact schedule: the kernel evaluates GaitGenerator.mpc_gait
+        (gait_generator.py:216-252) from the phase and SSP/DSP durations at every run()."""
+        self._gait = (_f32(gait_phase, self.device),
+                      ssp_durations.to(device=self.device, dtype=torch.int32).contiguous(),
+                      dsp_durations.to(device=self.device, dtype=torch.int32).contiguous())
+
+    def set_mpc_sampling_time(self, dt_mpc: torch.Tensor) -> None:
+        self.dt_mpc = dt_mpc
+
+    def reset(self, env_ids: torch.Tensor) -> None:
+        self.first_run[env_ids] = True
+
+
+class MPCControllerHIP(BaseMPCController):
+    """Drop-in for MPCControllerCusadi: same construction and run() contract, HIP kernels only."""
+
+    def init_solver(self):
+        N, B, dev = self.horizon_length, self.num_envs, self.device
+        d = Dims(N)
+        self.former_inputs = [torch.empty((B, w), dtype=torch.float64, device=dev) for w in d.former_in_nnz]
+        self.buffers = solver.MPCSolveBuffers.allocate(N, B, dev)
+        self.foot_wrench = torch.empty((B, 2, 6), dtype=torch.float32, device=dev)
+        self.cost = torch.zeros(B, device=dev)
+        return self
+
+    def _prep_struct(self, keep: list) -> _native.MPCPrep:
+        st, ds, dev = self.state_estimate_data, self.desired_state_data, self.device
+        if st is None or ds is None:
+            raise RuntimeError("set_state_estimate_data / set_desired_state_data before run()")
+
+        def ptr(t):
+            keep.append(t)
+            return t.data_ptr()
+
+        p = _native.MPCPrep()
+        p.root_euler = ptr(_f32(st.root_euler, dev))
+        p.root_position = ptr(_f32(st.root_position, dev))
+        p.root_angular_velocity_w = ptr(_f32(st.root_angular_velocity_w, dev))
+        p.root_velocity_w = ptr(_f32(st.root_velocity_w, dev))
+        p.rotation_body = ptr(_f32(st.rotation_body, dev))
+        p.foot_position = ptr(_f32(st.foot_position, dev))
+        p.desired_velocity_b = ptr(_f32(ds.desired_velocity_b, dev))
+        p.desired_angular_velocity_b = ptr(_f32(ds.desired_angular_velocity_b, dev))
+        p.desired_height = ptr(_f32(ds.desired_height, dev))
+        for name in ("world_position_desired", "yaw_desired"):  # updated in place by the kernel
+            t = getattr(self, name)
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+                setattr(self, name, _f32(t, dev))
+        if self.first_run.dtype != torch.bool or not self.first_run.is_contiguous():
+            self.first_run = self.first_run.to(device=dev, dtype=torch.bool).contiguous()
+        p.world_position_desired = ptr(self.world_position_desired)
+        p.yaw_desired = ptr(self.yaw_desired)
+        p.first_run = ptr(self.first_run)
+        if self._gait is not None:
+            p.gait_phase, p.ssp_durations, p.dsp_durations = (ptr(t) for t in self._gait)
+        else:
+            p.contact_table = ptr(_f32(self.contact_table, dev))
+        p.dt_mpc = ptr(_f32(self.dt_mpc, dev))
+        p.residual_lin_accel = ptr(_f32(self.residual_lin_accel, dev))
+        p.residual_ang_accel = ptr(_f32(self.residual_ang_accel, dev))
+        p.I_body[:] = [float(v) for v in self.I_body.reshape(-1).tolist()]
+        p.mass, p.mu = float(self.mass), float(self.mu)
+        q = [float(v) for v in torch.as_tensor(self.Q, dtype=torch.float32).reshape(-1).tolist()]
+        if len(q) not in (12, 13):
+            raise ValueError("Q must have 12 (or the reference config's 13) entries")
+        p.Q[:len(q)] = q
+        p.q_len = len(q)
+        p.R[:] = [float(v) for v in torch.as_tensor(self.R, dtype=torch.float32).reshape(-1).tolist()]
+        # torch evaluates `decimation * dt * tensor` with the Python product cast to float32
+        p.step_dt = float(torch.tensor(self.cfg.decimation * self.cfg.dt, dtype=torch.float32))
+        p.literal_layout = 1 if self.cfg.literal_layout else 0
+        return p
+
+    def prepare(self) -> list[torch.Tensor]:
+        """Write the 17 qp_former inputs for this step (and advance the knot-point state)."""
+        keep: list = []
+        p = self._prep_struct(keep)
+        rc = _native.lib().srbd_prepare_inputs(
+            self.horizon_length, self.num_envs, ctypes.byref(p),
+            _native.ptr_array([t.data_ptr() for t in self.former_inputs]), solver._stream_ptr())
+        _native.check(rc, "srbd_prepare_inputs")
+        return self.former_inputs
+
+    def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        N = self.horizon_length
+        self.prepare()
+        out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
+        self.solution = out
+        rot = _f32(self.state_estimate_data.rotation_body, self.device)
+        rc = _native.lib().srbd_u0_wrench(N, self.num_envs, out[0].data_ptr(), rot.data_ptr(),
+                                          self.foot_wrench.data_ptr(), solver._stream_ptr())
+        _native.check(rc, "srbd_u0_wrench")
+        return self.foot_wrench, self.cost
+
+
+# the reference's class name, for drop-in imports
+MPCControllerCusadi = MPCControllerHIP
+
+
+def dense_scatter(values: torch.Tensor, inverse_index: torch.Tensor, shape: tuple[int, int],
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """(B, nnz) nonzeros -> (B, rows, cols) dense through ``inverse_index`` (int32 (rows*cols,),
+    nonzero index or -1) with one scatter kernel (CusadiFunction.getDenseOutput replacement)."""
+    B, nnz = values.shape
+    rc = shape[0] * shape[1]
+    if out is None:
+        out = torch.empty((B, shape[0], shape[1]), dtype=torch.float64, device=values.device)
+    vals = values.contiguous()
+    for lo in range(0, B, 65535):  # grid.y limit per launch
+        hi = min(B, lo + 65535)
+        rc_ = _native.lib().srbd_dense_scatter(hi - lo, nnz, rc, inverse_index.data_ptr(),
+                                               vals[lo:hi].data_ptr(), out[lo:hi].data_ptr(),
+                                               solver._stream_ptr())
+        _native.check(rc_, "srbd_dense_scatter")
+    return out
+
+
+def inverse_index(rows, cols, shape: tuple[int, int], device) -> torch.Tensor:
+    """Dense position -> nonzero index map of a sparsity given as triplets (-1 = structural zero)."""
+    inv = torch.full((shape[0] * shape[1],), -1, dtype=torch.int32)
+    lin = torch.as_tensor(rows, dtype=torch.int64) * shape[1] + torch.as_tensor(cols, dtype=torch.int64)
+    inv[lin] = torch.arange(lin.numel(), dtype=torch.int32)
+    return inv.to(device)

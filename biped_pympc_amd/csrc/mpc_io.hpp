@@ -1,0 +1,211 @@
+// mpc_io.hpp -- the MPC step's input preparation, output post-processing and dense-output kernels
+// (SURVEY.md §8(a) a12/a13, §8(f) rows 1-3).
+//
+// prepare_inputs_kernel: per env, the controller-side preparation the reference runs as ~40 small
+//   FP32 torch ops before qp_former -- BaseMPCController.compute_knot_points / set_initial_state /
+//   compute_reference_trajectory (base_controller.py:166-257), GaitGenerator.mpc_gait
+//   (gait_generator.py:216-252) and the input assembly of MPCControllerCusadi.run
+//   (mpc_controller_cusadi.py:54-95) -- fused into one thread per env that writes the 17 FP64
+//   former inputs. FP32 arithmetic follows the torch op sequence: every torch op rounds, so products
+//   and sums are evaluated with FP contraction off (no FMA).
+// u0_wrench_kernel: u0 -> body-frame foot wrench, mpc_controller_cusadi.py:186-203.
+// dense_scatter_kernel: CCS nonzeros -> dense (B, rows, cols), CusadiFunction.getDenseOutput
+//   (CusadiFunction.py:49-58) as a direct scatter from an inverse index map.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srbd {
+
+struct PrepArgs {
+  // robot state estimate (float32): (B,3) x4, rotation (B,3,3) row-major, feet (B,2,3)
+  const float *root_euler, *root_position, *ang_vel_w, *vel_w, *rotation_body, *foot_position;
+  // command (float32): desired body velocity (B,3), angular velocity (B,3), height (B)
+  const float *des_vel_b, *des_angvel_b, *des_height;
+  // controller state, updated in place: world_position_desired (B,3), yaw_desired (B), first_run
+  float *wpd, *yaw_des;
+  uint8_t* first_run;
+  // contact schedule: gait phase (B) + SSP/DSP durations (B,2) int32, or an explicit (B,N,2) table
+  const float* gait_phase;
+  const int32_t *ssp, *dsp;
+  const float* contact_table;
+  // per-env parameters (float32): dt_mpc (B), residual accelerations (B,3) x2
+  const float *dt_mpc, *res_lin, *res_ang;
+  float I_body[9];
+  double mass, mu;
+  float Q[13], R[12];
+  int q_len;       // entries of the configured Q (MPCConf.Q has 13)
+  float step_dt;   // float32(decimation * dt): open-loop knot advance per MPC update
+  int literal;     // 1: reference GPU-caller flattening; 0: corrected layout
+  double* out[17];
+  int N, batch;
+};
+
+// One rounding per torch op: hipcc contracts a*b+c into an FMA by default (-ffp-contract=fast) and
+// HIP's __fmul_rn/__fadd_rn are plain operations, so contraction is switched off where they live.
+__device__ __forceinline__ float fm(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float fa(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+// (M v)_i of a 3x3 row-major FP32 matrix as a batched matmul of one row: ((m0 v0 + m1 v1) + m2 v2)
+__device__ __forceinline__ float dot3f(float m0, float m1, float m2, float v0, float v1, float v2) {
+#pragma clang fp contract(off)
+  return (m0 * v0 + m1 * v1) + m2 * v2;
+}
+
+__global__ __launch_bounds__(256) void prepare_inputs_kernel(PrepArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.batch) return;
+  const int N = a.N;
+  double* const* o = a.out;
+  const float* rp = a.root_position + 3 * e;
+  const float* eu = a.root_euler + 3 * e;
+  // compute_knot_points (base_controller.py:166-176)
+  float w0 = a.wpd[3 * e], w1 = a.wpd[3 * e + 1], w2 = a.wpd[3 * e + 2], yaw = a.yaw_des[e];
+  if (a.first_run[e]) {
+    w0 = rp[0];
+    w1 = rp[1];
+    w2 = rp[2];
+    yaw = eu[2];
+    a.first_run[e] = 0;
+  }
+  // set_initial_state (:201-211) -> x0 (input 0)
+  double* x0 = o[0] + (size_t)e * 12;
+  for (int j = 0; j < 3; ++j) {
+    x0[j] = eu[j];
+    x0[3 + j] = rp[j];
+    x0[6 + j] = a.ang_vel_w[3 * e + j];
+    x0[9 + j] = a.vel_w[3 * e + j];
+  }
+  // compute_reference_trajectory (:213-257)
+  const float* vb = a.des_vel_b + 3 * e;
+  const float wz = a.des_angvel_b[3 * e + 2], h = a.des_height[e], dt = a.dt_mpc[e];
+  w0 = fa(w0, fm(a.step_dt, vb[0]));
+  w1 = fa(w1, fm(a.step_dt, vb[1]));
+  w2 = h;
+  yaw = fa(yaw, fm(a.step_dt, wz));
+  const bool stationary = fabsf(vb[0]) < 1e-2f;
+  const float* Rm = a.rotation_body + 9 * e;
+  const float vw0 = dot3f(Rm[0], Rm[1], Rm[2], vb[0], vb[1], vb[2]);
+  const float vw1 = dot3f(Rm[3], Rm[4], Rm[5], vb[0], vb[1], vb[2]);
+  const float px = stationary ? w0 : rp[0], py = stationary ? w1 : rp[1];
+  double* xr = o[3] + (size_t)e * 12 * N;
+  for (int k = 0; k < N; ++k) {
+    const float t = fm(dt, (float)k);
+    double* r = xr + 12 * k;
+    r[0] = 0.0;
+    r[1] = 0.0;
+    r[2] = fa(yaw, fm(wz, t));
+    r[3] = fa(px, fm(vw0, t));
+    r[4] = fa(py, fm(vw1, t));
+    r[5] = h;
+    r[6] = 0.0;
+    r[7] = 0.0;
+    r[8] = wz;
+    r[9] = vw0;
+    r[10] = vw1;
+    r[11] = 0.0;
+  }
+  a.wpd[3 * e] = w0;
+  a.wpd[3 * e + 1] = w1;
+  a.wpd[3 * e + 2] = w2;
+  a.yaw_des[e] = yaw;
+  // linearisation points x, u = ones (mpc_controller_cusadi.py:55-56)
+  for (int j = 0; j < 12 * N; ++j) {
+    o[1][(size_t)e * 12 * N + j] = 1.0;
+    o[2][(size_t)e * 12 * N + j] = 1.0;
+  }
+  o[4][e] = (double)dt;
+  o[5][e] = a.mass;
+  o[6][e] = a.mu;
+  // R_body (:58): row-major flattening (literal; CasADi decodes it column-major) or column-major
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) o[7][(size_t)e * 9 + (a.literal ? 3 * i + j : 3 * j + i)] = Rm[3 * i + j];
+  // I_world = R I_body R^T as two FP32 batched matmuls (:59-61)
+  float T[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      T[3 * i + j] = dot3f(Rm[3 * i], Rm[3 * i + 1], Rm[3 * i + 2], a.I_body[j], a.I_body[3 + j], a.I_body[6 + j]);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      o[8][(size_t)e * 9 + 3 * i + j] = dot3f(T[3 * i], T[3 * i + 1], T[3 * i + 2], Rm[3 * j], Rm[3 * j + 1], Rm[3 * j + 2]);
+  for (int j = 0; j < 3; ++j) {
+    o[9][(size_t)e * 3 + j] = rp[j];
+    o[10][(size_t)e * 3 + j] = a.foot_position[6 * e + j];
+    o[11][(size_t)e * 3 + j] = a.foot_position[6 * e + 3 + j];
+    o[15][(size_t)e * 3 + j] = a.res_lin[3 * e + j];
+    o[16][(size_t)e * 3 + j] = a.res_ang[3 * e + j];
+  }
+  // contact schedule: GaitGenerator.mpc_gait (gait_generator.py:216-252) or the given table;
+  // flattened (N,2) row-major as the caller does (:65; literal) or column-major (corrected)
+  double* ct = o[12] + (size_t)e * 2 * N;
+  if (a.gait_phase) {
+    const int s0 = a.ssp[2 * e], s1 = a.ssp[2 * e + 1], d0 = a.dsp[2 * e], d1 = a.dsp[2 * e + 1];
+    const int cyc = s0 + s1 + d0 + d1;
+    const int g = (int)fm(a.gait_phase[e], (float)cyc);  // (phase * cycle).int(): truncation
+    for (int k = 0; k < N; ++k) {
+      if (cyc <= 0) {  // degenerate durations (torch would fault on % 0): double support
+        ct[a.literal ? 2 * k : k] = 1.0;
+        ct[a.literal ? 2 * k + 1 : N + k] = 1.0;
+        continue;
+      }
+      int st = (g + k) % cyc;
+      if (st < 0) st += cyc;  // torch remainder takes the divisor's sign
+      const bool p1 = st < s1, p2 = st >= s1 && st < s1 + d0, p3 = st >= s1 + d0 && st < s1 + d0 + s0;
+      const bool fin = !(p1 || p2 || p3);
+      const double cl = (p1 || p2 || fin) ? 1.0 : 0.0, cr = (p2 || p3 || fin) ? 1.0 : 0.0;
+      ct[a.literal ? 2 * k : k] = cl;
+      ct[a.literal ? 2 * k + 1 : N + k] = cr;
+    }
+  } else {
+    for (int k = 0; k < N; ++k) {
+      ct[a.literal ? 2 * k : k] = a.contact_table[(size_t)e * 2 * N + 2 * k];
+      ct[a.literal ? 2 * k + 1 : N + k] = a.contact_table[(size_t)e * 2 * N + 2 * k + 1];
+    }
+  }
+  // Q, R (:70-71). The caller hands a (B, 13) Q to an input read with stride 12, so env e sees
+  // Q[(12 e + j) mod 13]; that is written here into a well-formed (B, 12).
+  for (int j = 0; j < 12; ++j) {
+    const int qi = (a.literal && a.q_len == 13) ? (int)(((long long)12 * e + j) % 13) : j;
+    o[13][(size_t)e * 12 + j] = a.Q[qi];
+    o[14][(size_t)e * 12 + j] = a.R[j];
+  }
+}
+
+// u0 -> body-frame foot wrench (float32, (B, 2, 6)): mpc_controller_cusadi.py:186-203
+__global__ __launch_bounds__(256) void u0_wrench_kernel(int N, int batch, const double* __restrict__ x,
+                                                        const float* __restrict__ rotation_body,
+                                                        float* __restrict__ wrench) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= batch) return;
+  const double* u0 = x + (size_t)e * 24 * N + 12 * N;
+  float u[12];
+  for (int j = 0; j < 12; ++j) u[j] = (float)u0[j];
+  u[6] = 0.0f;  // left_grm[:, 0] = 0
+  u[9] = 0.0f;  // right_grm[:, 0] = 0
+  const float* Rm = rotation_body + 9 * e;
+  float* w = wrench + (size_t)e * 12;
+  // R^T v, then negate; blocks [lf, lm | rf, rm] with u = [lf(0..2), rf(3..5), lm(6..8), rm(9..11)]
+  const int src[4] = {0, 6, 3, 9};
+  for (int b = 0; b < 4; ++b) {
+    const float* v = u + src[b];
+    for (int i = 0; i < 3; ++i) w[3 * b + i] = -dot3f(Rm[i], Rm[3 + i], Rm[6 + i], v[0], v[1], v[2]);
+  }
+}
+
+// dense (B, rc) from CCS nonzeros (B, nnz) through inv[rc] (nonzero index or -1)
+__global__ __launch_bounds__(256) void dense_scatter_kernel(int rc, int nnz, int batch, const int32_t* __restrict__ inv,
+                                                            const double* __restrict__ vals,
+                                                            double* __restrict__ dense) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = blockIdx.y;
+  if (idx >= rc || e >= batch) return;
+  const int k = inv[idx];
+  dense[(size_t)e * rc + idx] = k >= 0 ? vals[(size_t)e * nnz + k] : 0.0;
+}
+
+}  // namespace srbd

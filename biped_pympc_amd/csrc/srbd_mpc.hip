@@ -14,6 +14,7 @@
 #include "pdipm_srbd.hpp"
 #include "pdipm_srbd_reg.hpp"
 #include "qp_former.hpp"
+#include "mpc_io.hpp"
 
 namespace {
 
@@ -315,6 +316,80 @@ int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind) {
   }
   for (int c = 0; c < nz; ++c) colptr[c + 1] += colptr[c];
   return nnz;
+}
+
+int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* p, double* const* former_inputs,
+                        void* stream) {
+  if (!horizon_ok(horizon) || batch < 0 || !p || !former_inputs)
+    return set_error(kErrInvalid, "srbd_prepare_inputs: bad arguments");
+  if (batch == 0) return 0;
+  if (!p->root_euler || !p->root_position || !p->root_angular_velocity_w || !p->root_velocity_w ||
+      !p->rotation_body || !p->foot_position || !p->desired_velocity_b || !p->desired_angular_velocity_b ||
+      !p->desired_height || !p->world_position_desired || !p->yaw_desired || !p->first_run || !p->dt_mpc ||
+      !p->residual_lin_accel || !p->residual_ang_accel ||
+      (p->gait_phase ? (!p->ssp_durations || !p->dsp_durations) : !p->contact_table) ||
+      (p->q_len != 12 && p->q_len != 13))
+    return set_error(kErrInvalid, "srbd_prepare_inputs: missing array or bad q_len");
+  srbd::PrepArgs a{};
+  a.root_euler = p->root_euler;
+  a.root_position = p->root_position;
+  a.ang_vel_w = p->root_angular_velocity_w;
+  a.vel_w = p->root_velocity_w;
+  a.rotation_body = p->rotation_body;
+  a.foot_position = p->foot_position;
+  a.des_vel_b = p->desired_velocity_b;
+  a.des_angvel_b = p->desired_angular_velocity_b;
+  a.des_height = p->desired_height;
+  a.wpd = p->world_position_desired;
+  a.yaw_des = p->yaw_desired;
+  a.first_run = p->first_run;
+  a.gait_phase = p->gait_phase;
+  a.ssp = p->ssp_durations;
+  a.dsp = p->dsp_durations;
+  a.contact_table = p->contact_table;
+  a.dt_mpc = p->dt_mpc;
+  a.res_lin = p->residual_lin_accel;
+  a.res_ang = p->residual_ang_accel;
+  std::memcpy(a.I_body, p->I_body, sizeof(a.I_body));
+  a.mass = p->mass;
+  a.mu = p->mu;
+  std::memcpy(a.Q, p->Q, sizeof(a.Q));
+  a.q_len = p->q_len;
+  std::memcpy(a.R, p->R, sizeof(a.R));
+  a.step_dt = p->step_dt;
+  a.literal = p->literal_layout ? 1 : 0;
+  for (int i = 0; i < 17; ++i) {
+    if (!former_inputs[i]) return set_error(kErrInvalid, "srbd_prepare_inputs: null output");
+    a.out[i] = former_inputs[i];
+  }
+  a.N = horizon;
+  a.batch = batch;
+  hipLaunchKernelGGL(srbd::prepare_inputs_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "prepare_inputs_kernel launch");
+}
+
+int srbd_u0_wrench(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
+                   void* stream) {
+  if (!horizon_ok(horizon) || batch < 0 || (batch > 0 && (!x || !rotation_body || !foot_wrench)))
+    return set_error(kErrInvalid, "srbd_u0_wrench: bad arguments");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(srbd::u0_wrench_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, horizon,
+                     batch, x, rotation_body, foot_wrench);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "u0_wrench_kernel launch");
+}
+
+int srbd_dense_scatter(int batch, int nnz, int rc, const int* inverse_index, const double* values, double* dense,
+                       void* stream) {
+  if (batch < 0 || nnz < 0 || rc < 0 || batch > 65535 ||
+      (batch > 0 && rc > 0 && (!inverse_index || !dense || (nnz > 0 && !values))))
+    return set_error(kErrInvalid, "srbd_dense_scatter: bad arguments (batch <= 65535 per call)");
+  if (batch == 0 || rc == 0) return 0;
+  hipLaunchKernelGGL(srbd::dense_scatter_kernel, dim3((rc + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, rc,
+                     nnz, batch, (const int32_t*)inverse_index, values, dense);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "dense_scatter_kernel launch");
 }
 
 }  // extern "C"

@@ -9,7 +9,7 @@ deliberate:
   * a failing kernel raises ``RuntimeError`` with the library's message instead of the reference's
     ``exit(code)`` inside ``gpuErrchk`` (``generateCUDACode.py:106-112``);
   * the device pointer tables are refreshed with one host->device copy instead of one per element,
-    and ``getDenseOutput`` caches its scatter indices (same results).
+    and ``getDenseOutput`` is one scatter kernel over a cached index map (same results).
 As in the reference, the caller's tensors are used in place through ``data_ptr()`` and their
 strides are NOT consulted: pass contiguous ``(num_instances, nnz_in[i])`` FP64 CUDA tensors.
 """
@@ -22,6 +22,7 @@ import sys
 import torch
 
 from biped_pympc_amd.build import LIB_DIR, build_dropin
+from biped_pympc_amd.controller import dense_scatter, inverse_index
 
 
 class CusadiFunction:
@@ -66,17 +67,16 @@ class CusadiFunction:
         self.eval_time = t
 
     def getDenseOutput(self, out_idx=None):
+        """(B, size1, size2) dense output, scattered by one HIP kernel from the nonzeros through a
+        cached dense -> nonzero index map (the reference builds a COO tensor from Python lists
+        and calls .to_dense() on every call, CusadiFunction.py:49-58)."""
         fn = self.fn_casadi
+        s1, s2 = fn.size1_out(out_idx), fn.size2_out(out_idx)
         if out_idx not in self._dense_index:
             rows, cols = fn.sparsity_out(out_idx).get_triplet()
-            lin = torch.tensor(rows, dtype=torch.int64) * fn.size2_out(out_idx) + torch.tensor(cols, dtype=torch.int64)
-            self._dense_index[out_idx] = lin.to(self._device)
-        lin = self._dense_index[out_idx]
-        s1, s2 = fn.size1_out(out_idx), fn.size2_out(out_idx)
-        dense = torch.zeros((self.num_instances, s1 * s2), device=self._device, dtype=torch.double)
-        # sums duplicates like the reference's sparse_coo_tensor(...).to_dense() (there are none)
-        dense.index_add_(1, lin, self.outputs_sparse[out_idx].reshape(self.num_instances, -1))
-        return dense.view(self.num_instances, s1, s2)
+            self._dense_index[out_idx] = inverse_index(rows, cols, (s1, s2), self._device)
+        return dense_scatter(self.outputs_sparse[out_idx].reshape(self.num_instances, -1),
+                             self._dense_index[out_idx], (s1, s2))
 
     def checkInputDimensions(self, inputs):
         """Shape check of every input (the reference runs one CPU CasADi call, :60-67)."""

@@ -88,6 +88,61 @@ int srbd_set_solver_path(int path);
  * Returns nnz, or a negative value if the kernel's offsets are not a bijection onto a sorted CCS. */
 int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind);
 
+/* ---- MPC step around the QP ------------------------ */
+
+/* Everything BaseMPCController / MPCControllerCusadi assemble on the host before qp_former, as
+ * device arrays (float32 unless noted, batch-major). Field groups mirror the reference data
+ * classes: StateEStimatorData and DesiredStateData (core/data/robot_data.py:9-60), the controller's
+ * own knot-point state (base_controller.py:48,71-72), GaitGenerator (gait_generator.py:4-76) and
+ * MPCConf / the robot model (configuration.py:23-57, core/robot/hector.py:33-38). */
+typedef struct srbd_mpc_prep {
+  const float* root_euler;                 /* (B,3) */
+  const float* root_position;              /* (B,3) */
+  const float* root_angular_velocity_w;    /* (B,3) */
+  const float* root_velocity_w;            /* (B,3) */
+  const float* rotation_body;              /* (B,3,3) row-major */
+  const float* foot_position;              /* (B,2,3) world frame, [left, right] */
+  const float* desired_velocity_b;         /* (B,3) */
+  const float* desired_angular_velocity_b; /* (B,3) */
+  const float* desired_height;             /* (B) */
+  float* world_position_desired;           /* (B,3) read + updated */
+  float* yaw_desired;                      /* (B)   read + updated */
+  unsigned char* first_run;                /* (B)   bool, read + cleared */
+  const float* gait_phase;                 /* (B) or NULL: then contact_table is used */
+  const int* ssp_durations;                /* (B,2) int32 [left, right] */
+  const int* dsp_durations;                /* (B,2) int32 */
+  const float* contact_table;              /* (B,N,2), used when gait_phase == NULL */
+  const float* dt_mpc;                     /* (B) */
+  const float* residual_lin_accel;         /* (B,3) */
+  const float* residual_ang_accel;         /* (B,3) */
+  float I_body[9];                         /* host constants: body inertia (row-major) */
+  double mass, mu;
+  float Q[13];                             /* MPCConf.Q (13 entries in the reference config) */
+  int q_len;                               /* 12 or 13 */
+  float R[12];
+  float step_dt;                           /* float32(decimation * dt) */
+  int literal_layout;                      /* 1 = the reference GPU caller's flattening of R_body,
+                                              contact_table and Q;
+                                              0 = corrected layout */
+} srbd_mpc_prep;
+
+/* Replaces compute_knot_points + set_initial_state + compute_reference_trajectory
+ * (base_controller.py:166-257), GaitGenerator.mpc_gait (gait_generator.py:216-252) and the input
+ * assembly of MPCControllerCusadi.run (mpc_controller_cusadi.py:54-95): writes the 17 qp_former
+ * inputs (FP64, (B, nnz_in[i]), Q well-formed 12 wide) and updates the knot-point state. */
+int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* prep, double* const* former_inputs,
+                        void* stream);
+
+/* u0 = x[:, 12N:12N+12] -> foot wrench (B,2,6) float32 in the body frame, x-moments zeroed and
+ * negated as mpc_controller_cusadi.py:186-203. rotation_body (B,3,3) float32 row-major. */
+int srbd_u0_wrench(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
+                   void* stream);
+
+/* CusadiFunction.getDenseOutput (CusadiFunction.py:49-58) as one scatter: dense (B, rc) row-major
+ * from nonzeros (B, nnz) through inverse_index[rc] (nonzero index of each dense entry, or -1). */
+int srbd_dense_scatter(int batch, int nnz, int rc, const int* inverse_index, const double* values,
+                       double* dense, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
