@@ -24,7 +24,8 @@ template <int N>
 struct RegLayout {
   static constexpr int nz = 24 * N, m = 16 * N, p = 14 * N, nx = 12 * N;
   static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 144, K0 = Gf + 64, K1 = K0 + 78,
-                       Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, DV = SG + 16,
+                       Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, TRI = SG + 16,
+                       DV = TRI + 10,
                        X = DV + 78 * N, Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N, total = DYm + 2 * N;
   static constexpr int SI = (m + 63) / 64, SE = (p + 63) / 64, SX = (nx + 63) / 64;
@@ -40,6 +41,73 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
+// ---- fused broadcast-FMA: v_fmac_f64_dpp row_newbcast:K (gfx90a+ 64-bit DPP on a VOP2 FMA) ----
+// acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
+// v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
+// they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
+// entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
+// block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
+#define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
+
+// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for all 12 j (j == K included; the
+// caller overwrites S[K] afterwards)
+#define SRBD_PIVOT_BLOCK(K)                                                                          \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%0", "%12", K) SRBD_FMAC_BC("%1", "%1", "%12", K)              \
+          SRBD_FMAC_BC("%2", "%2", "%12", K) SRBD_FMAC_BC("%3", "%3", "%12", K)                       \
+              SRBD_FMAC_BC("%4", "%4", "%12", K) SRBD_FMAC_BC("%5", "%5", "%12", K)                   \
+                  SRBD_FMAC_BC("%6", "%6", "%12", K) SRBD_FMAC_BC("%7", "%7", "%12", K)               \
+                      SRBD_FMAC_BC("%8", "%8", "%12", K) SRBD_FMAC_BC("%9", "%9", "%12", K)           \
+                          SRBD_FMAC_BC("%10", "%10", "%12", K) SRBD_FMAC_BC("%11", "%11", "%12", K) "s_nop 1\n" \
+      : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]), \
+        "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11])                                              \
+      : "v"(coef))
+__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k) {
+  switch (k) {
+    case 0: SRBD_PIVOT_BLOCK(0); break;
+    case 1: SRBD_PIVOT_BLOCK(1); break;
+    case 2: SRBD_PIVOT_BLOCK(2); break;
+    case 3: SRBD_PIVOT_BLOCK(3); break;
+    case 4: SRBD_PIVOT_BLOCK(4); break;
+    case 5: SRBD_PIVOT_BLOCK(5); break;
+    case 6: SRBD_PIVOT_BLOCK(6); break;
+    case 7: SRBD_PIVOT_BLOCK(7); break;
+    case 8: SRBD_PIVOT_BLOCK(8); break;
+    case 9: SRBD_PIVOT_BLOCK(9); break;
+    case 10: SRBD_PIVOT_BLOCK(10); break;
+    default: SRBD_PIVOT_BLOCK(11); break;
+  }
+}
+
+// sum_j c[j] * v(lane j) over the 12 rows of a 16-lane DPP row (three interleaved accumulators)
+__device__ __forceinline__ double dot_bc12(const double (&c)[12], double v) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%3", "%4", 0) SRBD_FMAC_BC("%1", "%3", "%5", 1) SRBD_FMAC_BC("%2", "%3", "%6", 2)
+      SRBD_FMAC_BC("%0", "%3", "%7", 3) SRBD_FMAC_BC("%1", "%3", "%8", 4) SRBD_FMAC_BC("%2", "%3", "%9", 5)
+      SRBD_FMAC_BC("%0", "%3", "%10", 6) SRBD_FMAC_BC("%1", "%3", "%11", 7) SRBD_FMAC_BC("%2", "%3", "%12", 8)
+      SRBD_FMAC_BC("%0", "%3", "%13", 9) SRBD_FMAC_BC("%1", "%3", "%14", 10) SRBD_FMAC_BC("%2", "%3", "%15", 11)
+      "s_nop 1\n"
+      : "+v"(a0), "+v"(a1), "+v"(a2)
+      : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
+        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));
+  return (a0 + a1) + a2;
+}
+
+// acc[i] += v[i](lane 6) c6 + v[i](lane 7) c7 + v[i](lane 8) c8 for 4 elements (the rows 6..8 term
+// of the Schur update X = C V)
+__device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x2, double& x3, double v0,
+                                               double v1, double v2, double v3, double c6, double c7,
+                                               double c8) {
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%4", "%8", 6) SRBD_FMAC_BC("%1", "%5", "%8", 6) SRBD_FMAC_BC("%2", "%6", "%8", 6)
+      SRBD_FMAC_BC("%3", "%7", "%8", 6) SRBD_FMAC_BC("%0", "%4", "%9", 7) SRBD_FMAC_BC("%1", "%5", "%9", 7)
+      SRBD_FMAC_BC("%2", "%6", "%9", 7) SRBD_FMAC_BC("%3", "%7", "%9", 7) SRBD_FMAC_BC("%0", "%4", "%10", 8)
+      SRBD_FMAC_BC("%1", "%5", "%10", 8) SRBD_FMAC_BC("%2", "%6", "%10", 8) SRBD_FMAC_BC("%3", "%7", "%10", 8)
+      "s_nop 1\n"
+      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8));
+}
+
 // Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r in lane r of a 16-lane
 // DPP row; lanes 12..15 shadow row 11), by Gauss-Jordan pivoting on the diagonal. Unlike sweep12 the
 // pivot row is not rescaled in place: every lane keeps its row unscaled together with a scale
@@ -53,16 +121,11 @@ __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (
   double sc = 1.0;
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
-    double pk[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) pk[j] = bc16(Sr[j], k);
-    const double id = rcp_nr(pk[k]);
+    const double id = rcp_nr(bc16(Sr[k], k));
     const bool piv = (r == k);
     const double ark = Sr[k];
     const double coef = piv ? 0.0 : -ark * id;
-#pragma unroll
-    for (int j = 0; j < 12; ++j)
-      if (j != k) Sr[j] = fma(coef, pk[j], Sr[j]);
+    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef (pk = row k, broadcast inside the FMA)
     Sr[k] = piv ? -1.0 : ark * id;
     sc = piv ? id : sc;
   }
@@ -224,6 +287,7 @@ struct RegCtx {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *DV = at(Lo::DV), *PHs = at(Lo::TV);  // PHs: scratch, TV is dead here
     const double *Gf = at(Lo::Gf), *Hu = at(Lo::Hu), *Nd = at(Lo::Nd), *K0 = at(Lo::K0), *K1 = at(Lo::K1);
+    const uint8_t* TRI = reinterpret_cast<const uint8_t*>(at(Lo::TRI));
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + 64 * t;
@@ -263,8 +327,8 @@ struct RegCtx {
     __syncthreads();
     for (int e = lane; e < 78 * N; e += 64) {  // S_ii = K + sum_f N_f Phi_f^-1 N_f^T
       const int i = e / 78, l = e % 78;
-      int r, c;
-      tri_rc(l, r, c);
+      const int rc = TRI[l];  // packed-lower position -> (row, col), table built once per kernel
+      const int r = rc & 15, c = rc >> 4;
       double v = (i == 0 ? K0 : K1)[l];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
@@ -303,6 +367,9 @@ struct RegCtx {
       const double cra0 = r < 3 ? cc[12 + 3 * r] : 0.0, cra1 = r < 3 ? cc[13 + 3 * r] : 0.0,
                    cra2 = r < 3 ? cc[14 + 3 * r] : 0.0;
       const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
+      int offs[12];  // packed-lower offset of (pr, column c in group coordinates)
+#pragma unroll
+      for (int c = 0; c < 12; ++c) offs[c] = sym_idx(pr, g ? perm12c(c) : c);
       double Dr[12];
 #pragma unroll
       for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
@@ -318,7 +385,7 @@ struct RegCtx {
         if (act) {
           const double* Si = DV + 78 * i;
 #pragma unroll
-          for (int c = 0; c < 12; ++c) Sr[c] = Si[sym_idx(pr, g ? perm12c(c) : c)];
+          for (int c = 0; c < 12; ++c) Sr[c] = Si[offs[c]];
           if (prev) {
             double V[12];
 #pragma unroll
@@ -329,11 +396,11 @@ struct RegCtx {
               V[c] = v;
             }
 #pragma unroll
-            for (int c = 0; c < 12; ++c) {
-              const double v = V[c];
-              X[c] = (crd * v + crb * shl6(v)) +
-                     ((cra0 * bc16(v, 6) + cra1 * bc16(v, 7)) + cra2 * bc16(v, 8));
-            }
+            for (int c = 0; c < 12; ++c) X[c] = crd * V[c] + crb * shl6(V[c]);
+#pragma unroll
+            for (int c = 0; c < 12; c += 4)  // + rows 6..8 of V through fused broadcast-FMAs
+              fmac_rows678_4(X[c], X[c + 1], X[c + 2], X[c + 3], V[c], V[c + 1], V[c + 2], V[c + 3], cra0, cra1,
+                             cra2);
             if (!(mstep && g == 1)) {
 #pragma unroll
               for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
@@ -354,7 +421,7 @@ struct RegCtx {
 #pragma unroll
             for (int c = 0; c < 12; ++c) {
               const int pc = g ? perm12c(c) : c;
-              if (pc <= pr) Di[pr * (pr + 1) / 2 + pc] = Dr[c];
+              if (pc <= pr) Di[offs[c]] = Dr[c];
             }
           }
         }
@@ -444,10 +511,12 @@ struct RegCtx {
       const int cnt = g ? nb : nf;
       const double* cc = at(Lo::Cc) + 24 * g;
       double Crow[12], Ccol[12];
+      int offs[12];
 #pragma unroll
       for (int j = 0; j < 12; ++j) {
         Crow[j] = cel(cc, r, j);
         Ccol[j] = cel(cc, j, r);
+        offs[j] = sym_idx(pr, g ? perm12c(j) : j);
       }
       double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
 #pragma unroll
@@ -459,32 +528,16 @@ struct RegCtx {
         const bool act = mstep ? true : (t < cnt);
         const bool prev = mstep ? (cnt >= 1) : (t >= 1);
         double cw = 0.0;
-        if (act && prev) {
-          double c0 = 0.0, c1 = 0.0, c2 = 0.0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            c0 += Crow[j] * bc16(w, j);
-            c1 += Crow[j + 4] * bc16(w, j + 4);
-            c2 += Crow[j + 8] * bc16(w, j + 8);
-          }
-          cw = (c0 + c1) + c2;
-        }
+        if (act && prev) cw = dot_bc12(Crow, w);
         double mv = 0.0;
         if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
         if (act && !(mstep && g == 1)) {
           const double* Di = DV + 78 * i;
           double Dr[12];
 #pragma unroll
-          for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12c(k) : k)];
+          for (int k = 0; k < 12; ++k) Dr[k] = Di[offs[k]];
           const double q = (QV[12 * i + pr] - cw) - mv;
-          double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            a0 += Dr[k] * bc16(q, k);
-            a1 += Dr[k + 4] * bc16(q, k + 4);
-            a2 += Dr[k + 8] * bc16(q, k + 8);
-          }
-          w = (a0 + a1) + a2;
+          w = dot_bc12(Dr, q);
 #pragma unroll
           for (int k = 0; k <= T; ++k) wv[k] = (k == t) ? w : wv[k];
         }
@@ -504,23 +557,9 @@ struct RegCtx {
           const double* Di = DV + 78 * i;
           double Dr[12];
 #pragma unroll
-          for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12c(k) : k)];
-          double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {  // Cg^T y_prev
-            s0 += Ccol[j] * bc16(y, j);
-            s1 += Ccol[j + 4] * bc16(y, j + 4);
-            s2 += Ccol[j + 8] * bc16(y, j + 8);
-          }
-          const double sc = (s0 + s1) + s2;
-          double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            a0 += Dr[k] * bc16(sc, k);
-            a1 += Dr[k + 4] * bc16(sc, k + 4);
-            a2 += Dr[k + 8] * bc16(sc, k + 8);
-          }
-          y = wprev - ((a0 + a1) + a2);
+          for (int k = 0; k < 12; ++k) Dr[k] = Di[offs[k]];
+          const double sc = dot_bc12(Ccol, y);  // Cg^T y_prev
+          y = wprev - dot_bc12(Dr, sc);
           if (own) QV[12 * i + pr] = y;
         }
       }
@@ -665,6 +704,11 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
     return;
   }
   // ---- per-QP constants ----
+  for (int l = lane; l < 78; l += 64) {  // packed-lower index -> (row | col << 4)
+    int r, c;
+    tri_rc(l, r, c);
+    reinterpret_cast<uint8_t*>(smem + Lo::TRI)[l] = (uint8_t)(r | (c << 4));
+  }
   if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
   if (lane == 0) {
     const double e6 = Ag[a_ubase(N) + c_tab.e6], e9 = Ag[a_ubase(N) + c_tab.e9];
