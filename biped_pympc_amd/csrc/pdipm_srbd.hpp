@@ -601,27 +601,14 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   }
   __syncthreads();
   if (lane < 28) C.Gd[c_tab.grow[lane] * 12 + c_tab.gcol[lane]] = Gg[lane];
-  // ---- stage-invariance check (bitwise) ----
+  // ---- stage-invariance check (bitwise): every periodic block equals the first one ----
   bool bad = false;
   for (int e = lane; e < nA; e += 64) {
-    double ref;
-    // locate e: x blocks, x_N singles, u blocks
-    if (e < 36 * (N - 1)) {
-      const int loc = e % 36;
-      int j = 11;
-      while (c_tab.cpx[j] > loc) --j;
-      const int t = loc - c_tab.cpx[j];
-      ref = (t == 0) ? C.Pd[j] : C.Md[c_tab.sx[j][t - 1] * 12 + j];
-    } else if (e < a_ubase(N)) {
-      ref = C.Pd[e - 36 * (N - 1)];
-    } else {
-      const int loc = (e - a_ubase(N)) % 86;
-      int j = 11;
-      while (c_tab.cpu[j] > loc) --j;
-      const int t = loc - c_tab.cpu[j];
-      ref = (t < c_tab.su_n[j]) ? C.Nd[c_tab.su[j][t] * 12 + j] : Ag[a_ubase(N) + loc];
-    }
-    bad |= !(Ag[e] == ref);
+    int ref;
+    if (e < 36 * (N - 1)) ref = e % 36;
+    else if (e < a_ubase(N)) ref = a_pidx(c_tab, N, 0, e - 36 * (N - 1));
+    else ref = a_ubase(N) + (e - a_ubase(N)) % 86;
+    bad |= !(Ag[e] == Ag[ref]);
   }
   for (int e = lane; e < nG; e += 64) bad |= !(Gg[e] == Gg[e % 28]);
   for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < 12 * N ? 0 : 12 * N) + e % 12]);
