@@ -44,6 +44,10 @@ struct Tables {
   int8_t gr_n[16];
   int8_t gr_off[16][2];
   int8_t gr_col[16][2];
+  // Inverse of cpx/cpu: (row, column) of each offset inside one x block (36) / u block (86);
+  // row -1 = the +I entry of an x column, row 12/13 = the x-moment entries e6/e9 of a u block.
+  int8_t xb_r[36], xb_j[36];
+  int8_t ub_r[86], ub_j[86];
   // Foot blocks of Phi_u: u columns {0,1,2,7} (left) and {3,4,5,10} (right).
   int8_t foot_col[2][4];
   // column -> (foot, position) or -1 for the four decoupled columns {6,8,9,11}
@@ -90,6 +94,22 @@ constexpr Tables make_tables() {
   }
   t.e6 = (int16_t)(t.cpu[6] + t.su_n[6]);
   t.e9 = (int16_t)(t.cpu[9] + t.su_n[9]);
+  for (int j = 0; j < 12; ++j) {
+    t.xb_r[t.cpx[j]] = -1;
+    t.xb_j[t.cpx[j]] = (int8_t)j;
+    for (int q = 0; q < t.sx_n[j]; ++q) {
+      t.xb_r[t.cpx[j] + 1 + q] = t.sx[j][q];
+      t.xb_j[t.cpx[j] + 1 + q] = (int8_t)j;
+    }
+    for (int q = 0; q < t.su_n[j]; ++q) {
+      t.ub_r[t.cpu[j] + q] = t.su[j][q];
+      t.ub_j[t.cpu[j] + q] = (int8_t)j;
+    }
+    if (j == 6 || j == 9) {
+      t.ub_r[t.cpu[j] + t.su_n[j]] = (int8_t)(j == 6 ? 12 : 13);
+      t.ub_j[t.cpu[j] + t.su_n[j]] = (int8_t)j;
+    }
+  }
   for (int r = 0; r < 12; ++r)
     for (int j = 0; j < 12; ++j) {
       t.Mi[r][j] = -1;
