@@ -71,6 +71,24 @@ def test_solver_matches_oracle(N, K, tol):
     assert u0_err.max() <= U0_TOL
 
 
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 32])
+def test_runtime_horizon_solver_matches_oracle(N):
+    """Horizons without a compile-time specialisation run the runtime-N LDS-resident kernel
+    (pdipm_srbd_kernel<0>), including the degenerate twisted recursions of N = 1, 2."""
+    B, K = 48, 5
+    wl = make_workload(B, N, seed=500 + N, random_gait=True)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    x, s, z, y = solver_init(d, N)
+    ins = [H, G, A, f, d, b, x, s, z, y]
+    ref = oracle.pdipm(N, K, ins)
+    out = solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K)
+    torch.cuda.synchronize()
+    for k in range(4):
+        o = out[k].cpu().numpy()
+        assert np.all(np.isfinite(o))
+        assert rel_err_rows(o, ref[k]).max() <= 1e-6, (N, k)
+
+
 def test_cold_start_matches_explicit_init():
     N, B, K = 10, 128, 10
     wl = make_workload(B, N, seed=7)
