@@ -41,6 +41,14 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
+// 1/d: v_rcp_f64 (~2^-24 relative) refined by one cubically convergent step y (1 + e + e^2),
+// e = 1 - d y: three dependent FMAs instead of two Newton steps' four (critical path of a pivot)
+__device__ __forceinline__ double rcp3(double d) {
+  const double y = __builtin_amdgcn_rcp(d);
+  const double e = fma(-d, y, 1.0);
+  return fma(y, fma(e, e, e), y);
+}
+
 // ---- fused broadcast-FMA: v_fmac_f64_dpp row_newbcast:K (gfx90a+ 64-bit DPP on a VOP2 FMA) ----
 // acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
 // v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
@@ -58,10 +66,23 @@ __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_d
                   SRBD_FMAC_BC("%6", "%6", "%12", K) SRBD_FMAC_BC("%7", "%7", "%12", K)               \
                       SRBD_FMAC_BC("%8", "%8", "%12", K) SRBD_FMAC_BC("%9", "%9", "%12", K)           \
                           SRBD_FMAC_BC("%10", "%10", "%12", K) SRBD_FMAC_BC("%11", "%11", "%12", K) "s_nop 1\n" \
-      : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]), \
-        "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11])                                              \
+      : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4), "+v"(s5), "+v"(s6), "+v"(s7), "+v"(s8),      \
+        "+v"(s9), "+v"(s10), "+v"(s11)                                                                \
       : "v"(coef))
-__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k) {
+// S[j] += S[j](lane k) * coef for every j except `skip`, whose operand slot takes `junk`
+__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k, int skip, double& junk) {
+  double& s0 = skip == 0 ? junk : S[0];
+  double& s1 = skip == 1 ? junk : S[1];
+  double& s2 = skip == 2 ? junk : S[2];
+  double& s3 = skip == 3 ? junk : S[3];
+  double& s4 = skip == 4 ? junk : S[4];
+  double& s5 = skip == 5 ? junk : S[5];
+  double& s6 = skip == 6 ? junk : S[6];
+  double& s7 = skip == 7 ? junk : S[7];
+  double& s8 = skip == 8 ? junk : S[8];
+  double& s9 = skip == 9 ? junk : S[9];
+  double& s10 = skip == 10 ? junk : S[10];
+  double& s11 = skip == 11 ? junk : S[11];
   switch (k) {
     case 0: SRBD_PIVOT_BLOCK(0); break;
     case 1: SRBD_PIVOT_BLOCK(1); break;
@@ -118,14 +139,14 @@ __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x
 //     lane k     : row unchanged except a_kk <- -1, scale <- id
 // On exit Dr[j] = (A^-1)_rj.
 __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (&Dr)[12]) {
-  double sc = 1.0;
+  double sc = 1.0, junk = 0.0;
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
-    const double id = rcp_nr(bc16(Sr[k], k));
+    const double id = rcp3(bc16(Sr[k], k));
     const bool piv = (r == k);
     const double ark = Sr[k];
     const double coef = piv ? 0.0 : -ark * id;
-    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef (pk = row k, broadcast inside the FMA)
+    pivot_update(Sr, coef, k, -1, junk);  // Sr[j] += pk[j] * coef (pk = row k, fused broadcast)
     Sr[k] = piv ? -1.0 : ark * id;
     sc = piv ? id : sc;
   }
@@ -521,7 +542,7 @@ struct RegCtx {
       double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
 #pragma unroll
       for (int k = 0; k <= T; ++k) wv[k] = 0.0;
-#pragma unroll 1
+#pragma unroll
       for (int t = 0; t <= T; ++t) {
         const bool mstep = (t == T);
         const int i = mstep ? mid : (g ? N - 1 - t : t);
@@ -546,7 +567,7 @@ struct RegCtx {
       const double ym = __shfl(w, perm12(r), 64);
       if (own && g == 0) QV[12 * mid + r] = w;
       double y = g ? ym : w;
-#pragma unroll 1
+#pragma unroll
       for (int t = 0; t < T; ++t) {
         const int i = g ? mid + 1 + t : mid - 1 - t;
         if (t < cnt) {

@@ -23,6 +23,9 @@ extern "C" __global__ void acc_kernel(const double* x, int n, unsigned long long
   atomicMax(&out[2], (unsigned long long)__double_as_longlong(e2));
   if (r1 != ex) atomicAdd(&out[3], 1ull);
   if (r2 != ex) atomicAdd(&out[4], 1ull);
+  const double e = fma(-d, r0, 1.0), r3 = fma(r0, fma(e, e, e), r0);  // cubic step (rcp3)
+  atomicMax(&out[5], (unsigned long long)__double_as_longlong(fabs(fma(d, r3, -1.0))));
+  if (r3 != ex) atomicAdd(&out[6], 1ull);
 }
 
 #define CHAIN 256

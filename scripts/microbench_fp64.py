@@ -21,7 +21,7 @@ n = 1 << 22
 rng = np.random.default_rng(0)
 x = np.exp(rng.uniform(np.log(1e-12), np.log(1e12), n)) * rng.choice([-1.0, 1.0], n)
 xd = torch.from_numpy(x).cuda()
-out = torch.zeros(5, dtype=torch.int64, device="cuda")
+out = torch.zeros(7, dtype=torch.int64, device="cuda")
 assert L.run_acc(ctypes.c_void_p(xd.data_ptr()), ctypes.c_int(n), ctypes.c_void_p(out.data_ptr())) == 0
 torch.cuda.synchronize()
 o = out.cpu().numpy()
@@ -29,6 +29,8 @@ f = [struct.unpack("<d", struct.pack("<q", int(v)))[0] for v in o[:3]]
 print(f"v_rcp_f64 accuracy over {n} log-uniform |x| in [1e-12, 1e12]:")
 print(f"  max |x r - 1|: raw {f[0]:.3e}, +1 Newton {f[1]:.3e}, +2 Newton {f[2]:.3e} (ulp(1) = 2.2e-16)")
 print(f"  r != correctly rounded 1/x: 1 Newton {o[3]} / {n}, 2 Newton {o[4]} / {n}")
+f3 = struct.unpack("<d", struct.pack("<q", int(o[5])))[0]
+print(f"  cubic step y(1+e+e^2): max |x r - 1| {f3:.3e}, != 1/x: {o[6]} / {n}")
 cyc = torch.zeros(10, dtype=torch.int64, device="cuda")
 sink = torch.zeros(64, dtype=torch.float64, device="cuda")
 for _ in range(2):
