@@ -211,6 +211,7 @@ struct RegCtx {
   static constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx;
   static constexpr int SI = Lo::SI, SE = Lo::SE, SX = Lo::SX;
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
+  static constexpr int kFactorUnroll = N <= 10 ? T + 1 : 1;
   double* L;
   int lane;
   const double *fg, *hg, *bg;
@@ -394,7 +395,8 @@ struct RegCtx {
       double Dr[12];
 #pragma unroll
       for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
-#pragma unroll 1
+      // fully unrolled at N = 10 (measured 1.5 % faster); the 11-step N = 20 chain stays rolled
+#pragma unroll kFactorUnroll
       for (int t = 0; t <= T; ++t) {
         const bool mstep = (t == T);
         const int i = mstep ? mid : (g ? N - 1 - t : t);
