@@ -32,11 +32,12 @@ from biped_pympc_amd.utils.synthetic import make_workload  # noqa: E402
 
 # Structural work per solve, frozen from scripts/algorithmic_work.py (SURVEY.md 8d convention:
 # the reference's sparse LDL^T of its 70N KKT per iteration; bytes = algorithmic HBM traffic).
+# bytes_fused = former inputs in + x, s, z, y, residuals, mu out (BASELINE.md "fused" bytes/solve).
 WORK = {
     10: {"flops_per_iter": 75840, "bytes_pdipm_cold": 23688, "bytes_step": 45352,
-         "bytes_former": 3616 + 18048},
+         "bytes_former": 3616 + 18048, "bytes_fused": 3616 + 5640},
     20: {"flops_per_iter": 165074, "bytes_pdipm_cold": 47528, "bytes_step": 90472,
-         "bytes_former": 6656 + 36288},
+         "bytes_former": 6656 + 36288, "bytes_fused": 6656 + 11240},
 }
 PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD spec; no sparsity)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -70,8 +71,9 @@ def event_time_ms(fn, reps: int) -> float:
 
 
 def solver_kernel_name(N: int) -> str:
-    """The stage-invariant solver kernel launch_solver picks for horizon N (srbd_mpc.hip)."""
-    return f"pdipm_srbd_reg_kernel<{N}>" if N in (10, 20) else "pdipm_srbd_kernel<0>"
+    """The kernel that runs the bench step at horizon N: the fused former + solver kernel for N = 10
+    and 20 (srbd_mpc_solve_fused), otherwise the runtime-N solver after qp_former."""
+    return f"mpc_step_reg_kernel<{N}>" if N in (10, 20) else "pdipm_srbd_kernel<0>"
 
 
 def load_pmc(N: int, B: int, K: int):
@@ -140,6 +142,10 @@ def main():
     ms_former = event_time_ms(lambda: solver.qp_former(inputs, N, outputs=qp), a.kernel_reps)
     ms_pdipm = event_time_ms(lambda: solver.pdipm(sol_qp, None, N, K, 1.0, outputs=pd_out),
                              a.kernel_reps)
+    # the step's own kernel: fused former + solver (N = 10, 20), timed on the same inputs
+    ms_fused = event_time_ms(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), a.kernel_reps)
+    fused = N in (10, 20)
+    ms_main = ms_fused if fused else ms_pdipm
     ms_gather = None
     if dist is not None:
         u0 = bufs.outputs[0][:, 12 * N:12 * N + 12]
@@ -149,20 +155,23 @@ def main():
     roofline = None
     if w is not None:
         flops = w["flops_per_iter"] * K * B
-        achieved = flops / (ms_pdipm * 1e-3) / 1e12
+        achieved = flops / (ms_main * 1e-3) / 1e12
+        hbm_bytes = (w["bytes_fused"] if fused else w["bytes_pdipm_cold"]) * B
         traffic, traffic_src = load_pmc(N, B, K)
         roofline = {
             "bound": "mfma", "kernel": solver_kernel_name(N), "achieved": round(achieved, 4),
             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
             "traffic": traffic, "traffic_source": traffic_src,
-            "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_pdipm, 4),
+            "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_main, 4),
             "note": ("FP64 compute roof (vector == matrix peak on MI355X); kernel runs on the "
                      "FP64 VALU. Flops = the reference's sparse-LDL KKT work per iteration "
-                     "(SURVEY 8d) x iterations x QPs per launch."),
-            "hbm": {"achieved_GBs": round(w["bytes_pdipm_cold"] * B / (ms_pdipm * 1e-3) / 1e9, 2),
+                     "(SURVEY 8d) x iterations x QPs per launch. Bytes = former inputs in + "
+                     "solution out per QP (fused step)." if fused else
+                     "FP64 compute roof; flops as SURVEY 8d; bytes = QP in + solution out."),
+            "hbm": {"achieved_GBs": round(hbm_bytes / (ms_main * 1e-3) / 1e9, 2),
                     "peak_GBs": PEAK_HBM_GBS,
-                    "frac": round(w["bytes_pdipm_cold"] * B / (ms_pdipm * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
-                    "algorithmic_bytes_per_launch": w["bytes_pdipm_cold"] * B},
+                    "frac": round(hbm_bytes / (ms_main * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
+                    "algorithmic_bytes_per_launch": hbm_bytes},
         }
 
     cpu = None
@@ -206,7 +215,8 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
                        "pdipm_iters": K, "qp_dims": [d.nz, d.n_eq, d.n_ineq],
                        "parallelism": f"dp{world}" + (" (u0 all_gather over RCCL)" if world > 1 else "")},
-            "kernels_ms": {"qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
+            "kernels_ms": {"mpc_step_fused": round(ms_fused, 4) if fused else None,
+                           "qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
                            "u0_all_gather": None if ms_gather is None else round(ms_gather, 4)},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -52,6 +52,8 @@ def lib() -> ctypes.CDLL:
     L.srbd_mpc_solve.restype = ctypes.c_int
     L.srbd_mpc_solve.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
                                  ctypes.c_void_p, P, ctypes.c_void_p]
+    L.srbd_mpc_solve_fused.restype = ctypes.c_int
+    L.srbd_mpc_solve_fused.argtypes = L.srbd_mpc_solve.argtypes
     L.srbd_evaluate_qp_former.restype = ctypes.c_float
     L.srbd_evaluate_qp_former.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]

@@ -17,6 +17,7 @@
 // [21 + r - 3] = (r, r + 6) for 3 <= r < 6 -- exactly the stage-coupling sparsity of -A_d.
 #pragma once
 #include "pdipm_srbd.hpp"
+#include "qp_former.hpp"
 
 namespace srbd {
 
@@ -660,61 +661,131 @@ struct RegCtx {
   }
 };
 
-template <int N>
-// N <= 10: 2 waves per SIMD (<= 256 registers); longer horizons: LDS allows 1 wave per SIMD anyway
-__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(SolverArgs args) {
+// Arguments of the fused former + solver kernel (srbd_mpc_solve_fused): the 17 qp_former inputs
+// in, the QP's vectors f, b, d written once (row per env, re-read by the same lanes every Newton
+// iteration; the matrices H, A, G never leave the kernel), the solver outputs out.
+struct FusedArgs {
+  const double* in[17];
+  double* vec[3];  // f (B, 24N), b (B, 14N), d (B, 16N)
+  double* out[6];  // x, s, z, y, residuals(4), mu(1)
+  int N, n_iter, batch;
+  double y0;
+};
+
+// Body shared by the solver kernel (kFused = false: the QP comes from qp_former's CCS outputs and is
+// checked for stage invariance) and the fused kernel (kFused = true: the stage blocks are computed
+// here from the former inputs with qp_former's own device code, invariant by construction).
+template <int N, bool kFused>
+__device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const FusedArgs& fa) {
   using Lo = RegLayout<N>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = blockIdx.x;
-  if (env >= args.batch) return;
+  if (env >= (kFused ? fa.batch : args.batch)) return;
   const int lane = threadIdx.x;
   constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
-  const int nA = nnz_A(N), nG = 28 * N;
   RegCtx<N> C;
   C.L = smem;
   C.lane = lane;
-  const double* Hg = solver_in(args, 0) + (size_t)env * nz;
-  const double* Gg = solver_in(args, 1) + (size_t)env * nG;
-  const double* Ag = solver_in(args, 2) + (size_t)env * nA;
-  C.fg = solver_in(args, 3) + (size_t)env * nz;
-  C.hg = solver_in(args, 4) + (size_t)env * m;
-  C.bg = solver_in(args, 5) + (size_t)env * p;
   double *Mc = smem + Lo::Mc, *Cc = smem + Lo::Cc, *Nd = smem + Lo::Nd, *Gf = smem + Lo::Gf,
          *K0 = smem + Lo::K0, *K1 = smem + Lo::K1, *Pd = smem + Lo::Pd, *IX = smem + Lo::IX,
          *Hu = smem + Lo::Hu, *SG = smem + Lo::SG;
-  double* Md = smem + Lo::TV;  // dense M while the constants are built (TV is free until solve)
+  double* Md = smem + Lo::X;  // dense M while the constants are built (X is set at the iterate init)
+  double e6 = 0.0, e9 = 0.0;  // x-moment coefficients (lane 0)
 
-  // ---- compact load (stage 0/1 slices) ----
-  for (int e = lane; e < 144; e += 64) {
-    const int r = e / 12, j = e % 12;
-    const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
-    Md[e] = (N >= 2 && om >= 0) ? Ag[a_xblock(1) + om] : 0.0;
-    Nd[e] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
-  }
-  Gf[lane] = 0.0;  // 64 entries
-  if (lane < 12) {
-    Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
-    Hu[lane] = Hg[nx + lane];
-    Hu[12 + lane] = Hg[lane];
-  }
-  __syncthreads();
-  if (lane < 28) Gf[4 * c_tab.grow[lane] + foot_pos(c_tab.gcol[lane])] = Gg[lane];
-  // ---- stage-invariance check (bitwise): every periodic block equals the first one ----
-  // x_k blocks (36 values, k = 1..N-1) vs x_1's; the x_N single entries vs x_1's +I entries (P);
-  // u_i blocks (86 values) vs u_0's (the latter include the x-moment entries e6/e9)
-  bool bad = false;
-  for (int e = lane; e < nA; e += 64) {
-    int ref;
-    if (e < 36 * (N - 1)) ref = e % 36;
-    else if (e < a_ubase(N)) ref = c_tab.cpx[e - 36 * (N - 1)];
-    else ref = a_ubase(N) + (e - a_ubase(N)) % 86;
-    bad |= !(Ag[e] == Ag[ref]);
-  }
-  for (int e = lane; e < nG; e += 64) bad |= !(Gg[e] == Gg[e % 28]);
-  for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
-  if (__any(bad)) {
-    if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
-    return;
+  if constexpr (kFused) {
+    // ---- the stage blocks from the former inputs (qp_former.hpp's former_model) ----
+    FormerLds& F = *reinterpret_cast<FormerLds*>(smem + Lo::TV);  // TV..DYm are free until the solve
+    static_assert(sizeof(FormerLds) <= sizeof(double) * (Lo::total - Lo::TV), "former scratch fits");
+    const int in_nnz[17] = {12, 12 * N, 12 * N, 12 * N, 1, 1, 1, 9, 9, 3, 3, 3, 2 * N, 12, 12, 3, 3};
+    const double* P[17];
+#pragma unroll
+    for (int i = 0; i < 17; ++i) P[i] = fa.in[i] + (size_t)env * in_nnz[i];
+    former_model(F, P, lane);
+    const double mu = P[6][0];
+    for (int e = lane; e < 144; e += 64) {
+      const int r = e / 12, j = e % 12;
+      const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
+      Md[e] = (N >= 2 && om >= 0) ? F.XB[om] : 0.0;
+      Nd[e] = on >= 0 ? F.UB[on] : 0.0;
+    }
+    Gf[lane] = 0.0;  // 64 entries
+    if (lane < 12) {
+      Pd[lane] = F.XB[c_tab.cpx[lane]];
+      Hu[lane] = P[14][lane];       // H = diag(Q.., R..): u part R
+      Hu[12 + lane] = P[13][lane];  // x part Q
+    }
+    if (lane == 0) {
+      e6 = F.UB[c_tab.e6];
+      e9 = F.UB[c_tab.e9];
+    }
+    __syncthreads();
+    if (lane < 28) Gf[4 * c_tab.grow[lane] + foot_pos(c_tab.gcol[lane])] = former_g(lane, mu);
+    // f, b, d rows, each entry written by the lane that reads it in residuals() / the cold init
+    double* fw = fa.vec[0] + (size_t)env * nz;
+    double* bw = fa.vec[1] + (size_t)env * p;
+    double* dw = fa.vec[2] + (size_t)env * m;
+#pragma unroll
+    for (int t = 0; t < Lo::SX; ++t) {
+      const int c = lane + 64 * t;
+      if (c < nx) {
+        fw[c] = former_f(c, N, P[13], P[14], P[1], P[2], P[3]);
+        fw[nx + c] = former_f(nx + c, N, P[13], P[14], P[1], P[2], P[3]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < Lo::SE; ++t)
+      if (lane + 64 * t < p) bw[lane + 64 * t] = former_b(lane + 64 * t, N, F);
+#pragma unroll
+    for (int t = 0; t < SI; ++t)
+      if (lane + 64 * t < m) dw[lane + 64 * t] = former_d(lane + 64 * t, N, P[2], P[12], mu);
+    __threadfence();
+    C.fg = fw;
+    C.bg = bw;
+    C.hg = dw;
+  } else {
+    const int nA = nnz_A(N), nG = 28 * N;
+    const double* Hg = solver_in(args, 0) + (size_t)env * nz;
+    const double* Gg = solver_in(args, 1) + (size_t)env * nG;
+    const double* Ag = solver_in(args, 2) + (size_t)env * nA;
+    C.fg = solver_in(args, 3) + (size_t)env * nz;
+    C.hg = solver_in(args, 4) + (size_t)env * m;
+    C.bg = solver_in(args, 5) + (size_t)env * p;
+    // ---- compact load (stage 0/1 slices) ----
+    for (int e = lane; e < 144; e += 64) {
+      const int r = e / 12, j = e % 12;
+      const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
+      Md[e] = (N >= 2 && om >= 0) ? Ag[a_xblock(1) + om] : 0.0;
+      Nd[e] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
+    }
+    Gf[lane] = 0.0;  // 64 entries
+    if (lane < 12) {
+      Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
+      Hu[lane] = Hg[nx + lane];
+      Hu[12 + lane] = Hg[lane];
+    }
+    if (lane == 0) {
+      e6 = Ag[a_ubase(N) + c_tab.e6];
+      e9 = Ag[a_ubase(N) + c_tab.e9];
+    }
+    __syncthreads();
+    if (lane < 28) Gf[4 * c_tab.grow[lane] + foot_pos(c_tab.gcol[lane])] = Gg[lane];
+    // ---- stage-invariance check (bitwise): every periodic block equals the first one ----
+    // x_k blocks (36 values, k = 1..N-1) vs x_1's; the x_N single entries vs x_1's +I entries (P);
+    // u_i blocks (86 values) vs u_0's (the latter include the x-moment entries e6/e9)
+    bool bad = false;
+    for (int e = lane; e < nA; e += 64) {
+      int ref;
+      if (e < 36 * (N - 1)) ref = e % 36;
+      else if (e < a_ubase(N)) ref = c_tab.cpx[e - 36 * (N - 1)];
+      else ref = a_ubase(N) + (e - a_ubase(N)) % 86;
+      bad |= !(Ag[e] == Ag[ref]);
+    }
+    for (int e = lane; e < nG; e += 64) bad |= !(Gg[e] == Gg[e % 28]);
+    for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
+    if (__any(bad)) {
+      if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
+      return;
+    }
   }
   // ---- per-QP constants ----
   for (int l = lane; l < 78; l += 64) {  // packed-lower index -> (row | col << 4)
@@ -724,7 +795,6 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
   }
   if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
   if (lane == 0) {
-    const double e6 = Ag[a_ubase(N) + c_tab.e6], e9 = Ag[a_ubase(N) + c_tab.e9];
     const double p6 = Hu[6] + kBeta, p9 = Hu[9] + kBeta;
     SG[0] = kDelta / (p6 * kDelta + e6 * e6);
     SG[1] = 1.0 / (Hu[8] + kBeta);
@@ -766,7 +836,7 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
   }
   // ---- iterate ----
   double *X = smem + Lo::X, *Z = smem + Lo::Z, *Y = smem + Lo::Y;
-  if (args.init_mode == 0) {
+  if (!kFused && args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;
@@ -793,7 +863,7 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
         Z[q] = 1.0;
       }
     }
-    for (int e = lane; e < p; e += 64) Y[e] = args.y0;
+    for (int e = lane; e < p; e += 64) Y[e] = kFused ? fa.y0 : args.y0;
   }
   __syncthreads();
 
@@ -803,7 +873,8 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
   const double* DYm = smem + Lo::DYm;
   const double* RXu = smem + Lo::RXu;
   PROF_MARK_CTX(C);
-  for (int it = 0; it < args.n_iter; ++it) {
+  const int n_iter = kFused ? fa.n_iter : args.n_iter;
+  for (int it = 0; it < n_iter; ++it) {
 #ifdef SRBD_REPEAT_PHASE  // diagnostic builds only (scripts/phase_ablation.py): run one idempotent
                           // phase twice so the timing difference is its marginal cost
     if (SRBD_REPEAT_PHASE == 1) (void)C.residuals();
@@ -849,7 +920,7 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
     }
     for (int e = ul; e < p; e += 64) Y[e] = Y[e] + adc * (e < nx ? QV[e] : DYm[e - nx]);
     mu_new = wave_sum(szn) / m;
-    if (it == args.n_iter - 1) {
+    if (it == n_iter - 1) {
       double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
       for (int t = 0; t < Lo::SX; ++t)
@@ -868,12 +939,13 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
     PROF_ADD_CTX(C, 5);
   }
   PROF_FLUSH(C);
-  double* xo = solver_out(args, 0) + (size_t)env * nz;
-  double* so = solver_out(args, 1) + (size_t)env * m;
-  double* zo = solver_out(args, 2) + (size_t)env * m;
-  double* yo = solver_out(args, 3) + (size_t)env * p;
-  double* ro = solver_out(args, 4) + (size_t)env * 4;
-  double* mo = solver_out(args, 5) + (size_t)env;
+  auto outp = [&](int k) { return kFused ? fa.out[k] : solver_out(args, k); };
+  double* xo = outp(0) + (size_t)env * nz;
+  double* so = outp(1) + (size_t)env * m;
+  double* zo = outp(2) + (size_t)env * m;
+  double* yo = outp(3) + (size_t)env * p;
+  double* ro = outp(4) + (size_t)env * 4;
+  double* mo = outp(5) + (size_t)env;
   for (int e = lane; e < nz; e += 64) xo[e] = X[e];
 #pragma unroll
   for (int t = 0; t < SI; ++t) {
@@ -891,6 +963,17 @@ __global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(S
     ro[3] = mu_new;
     mo[0] = mu_new;
   }
+}
+
+// N <= 10: 2 waves per SIMD (<= 256 registers); longer horizons: LDS allows 1 wave per SIMD anyway
+template <int N>
+__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(SolverArgs args) {
+  reg_kernel_body<N, false>(args, FusedArgs{});
+}
+
+template <int N>
+__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void mpc_step_reg_kernel(FusedArgs fa) {
+  reg_kernel_body<N, true>(SolverArgs{}, fa);
 }
 
 }  // namespace srbd

@@ -258,6 +258,46 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
   return srbd_pdipm_cold(horizon, n_iter, batch, y0, sin, outputs, stream);
 }
 
+int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                         double* qp_workspace, double* const* outputs, void* stream) {
+  if (!(horizon == 10 || horizon == 20) || g_solver_path != 0)  // no fused kernel: former + solver
+    return srbd_mpc_solve(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, stream);
+  if (n_iter < 1 || batch < 0 || !former_inputs || !qp_workspace || !outputs)
+    return set_error(kErrInvalid, "srbd_mpc_solve_fused: bad arguments");
+  if (batch == 0) return 0;
+  const size_t N = (size_t)horizon, B = (size_t)batch;
+  srbd::FusedArgs a{};
+  for (int i = 0; i < 17; ++i) {
+    if (!former_inputs[i]) return set_error(kErrInvalid, "srbd_mpc_solve_fused: null input");
+    a.in[i] = former_inputs[i];
+  }
+  for (int i = 0; i < 6; ++i) {
+    if (!outputs[i]) return set_error(kErrInvalid, "srbd_mpc_solve_fused: null output");
+    a.out[i] = outputs[i];
+  }
+  double* f = qp_workspace + B * 24 * N;   // same slots as srbd_mpc_solve's H, f, A, b, G, d
+  double* b = f + B * 24 * N + B * (122 * N - 24);
+  double* d = b + B * 14 * N + B * 28 * N;
+  a.vec[0] = f;
+  a.vec[1] = b;
+  a.vec[2] = d;
+  a.N = horizon;
+  a.n_iter = n_iter;
+  a.batch = batch;
+  a.y0 = y0;
+  static size_t cfg10 = 0, cfg20 = 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (horizon == 10) {
+    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, &cfg10)) return rc;
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(batch), dim3(64), kRegLds10, st, a);
+  } else {
+    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, &cfg20)) return rc;
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(batch), dim3(64), kRegLds20, st, a);
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");
+}
+
 int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind) {
   if (!horizon_ok(horizon) || !colptr || !rowind) return -1;
   constexpr srbd::Tables T = srbd::make_tables();

@@ -99,11 +99,14 @@ class MPCSolveBuffers:
 
 
 def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float = 1.0,
-              buffers: MPCSolveBuffers | None = None):
+              buffers: MPCSolveBuffers | None = None, fused: bool = True):
     """qp_former + cold-started PDIPM in one stream with no host synchronisation.
 
     Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
     iteration count as a runtime argument. Returns [x, s, z, y, residuals, mu].
+    ``fused`` (default): for N = 10 and 20 one kernel forms the QP's stage blocks in LDS and solves
+    it (``srbd_mpc_solve_fused``; only f, b, d reach ``buffers.workspace``); ``False`` runs the
+    former and the solver as two kernels with the full QP in the workspace.
     """
     d = Dims(N)
     B = former_inputs[0].shape[0]
@@ -111,7 +114,7 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     if buffers is None or buffers.B != B or buffers.N != N:
         buffers = MPCSolveBuffers.allocate(N, B, former_inputs[0].device)
     L = _native.lib()
-    rc = L.srbd_mpc_solve(N, n_iter, B, float(y0),
+    rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
                           _native.ptr_array([t.data_ptr() for t in former_inputs]),
                           buffers.workspace.data_ptr(),
                           _native.ptr_array([t.data_ptr() for t in buffers.outputs]), _stream_ptr())

@@ -73,6 +73,13 @@ size_t srbd_mpc_workspace_doubles(int horizon, int batch);
 int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                    double* qp_workspace, double* const* outputs, void* stream);
 
+/* srbd_mpc_solve in ONE kernel for N = 10 and 20 (other horizons, or a non-auto solver path, run
+ * srbd_mpc_solve): the stage blocks of H, A, G are computed in the solver from the former inputs
+ * and never written; f, b, d are written to their slots of the same qp_workspace and H, A, G slots
+ * are left untouched. Same outputs as srbd_mpc_solve. */
+int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                         double* qp_workspace, double* const* outputs, void* stream);
+
 /* LDS bytes one solver workgroup (one QP) uses at this horizon (0 if unsupported). */
 size_t srbd_solver_lds_bytes(int horizon);
 

@@ -30,6 +30,7 @@ def main():
     p.add_argument("--horizon", type=int, required=True)
     p.add_argument("--batch", type=int, required=True)
     p.add_argument("--iters", type=int, required=True)
+    p.add_argument("--kernel", default="mpc_step_reg_kernel", help="substring of the dominant kernel")
     a = p.parse_args()
     fetch, nf = per_kernel(a.fetch_csv, "FETCH_SIZE")
     write, _ = per_kernel(a.write_csv, "WRITE_SIZE")
@@ -40,8 +41,8 @@ def main():
         kernels[k] = {"dispatches": nf.get(k, 0), "fetch_size_raw_bytes": f_raw,
                       "fetch_bytes_corrected": 2.0 * f_raw, "write_bytes": w,
                       "hbm_bytes": 2.0 * f_raw + w}
-    # the solver kernel = the stage-invariant one that moved the most bytes
-    pd = sorted((v["hbm_bytes"], k) for k, v in kernels.items() if "pdipm_srbd" in k)
+    # the dominant kernel (by name substring) that moved the most bytes
+    pd = sorted((v["hbm_bytes"], k) for k, v in kernels.items() if a.kernel in k)
     out = {"horizon": a.horizon, "batch": a.batch, "iters": a.iters,
            "kernel": pd[-1][1] if pd else None,
            "pdipm_hbm_bytes_per_launch": pd[-1][0] if pd else None,

@@ -115,6 +115,20 @@ def test_mpc_solve_end_to_end():
     assert rel_err_rows(x, ref[0]).max() <= 1e-6
 
 
+@pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True)])
+def test_fused_step_equals_former_plus_solver(N, random_gait):
+    """srbd_mpc_solve_fused builds the stage blocks in the solver from the former inputs with the
+    former's own device code, so it reproduces former + solver bit for bit (N = 5 falls back)."""
+    B, K = 200, 10
+    wl = make_workload(B, N, seed=900 + N, random_gait=random_gait, residuals=random_gait)
+    ins = _cuda(wl.inputs)
+    fused = [t.clone() for t in solver.mpc_solve(ins, N, K, fused=True)]
+    plain = solver.mpc_solve(ins, N, K, fused=False)
+    torch.cuda.synchronize()
+    for a, c in zip(fused, plain):
+        assert torch.equal(a, c)
+
+
 def test_iteration_schedule_composes():
     """4 calls x 5 iterations (the reference GPU schedule, mpc_controller_cusadi.py:144-169) equal
     one call x 20 iterations: the solver keeps no hidden state."""
