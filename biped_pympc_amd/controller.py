@@ -6,12 +6,13 @@ Mirrors the reference controller API so a user of ``MPCControllerCusadi`` can sw
   * ``BaseMPCController`` setters and knot-point state (``convex_mpc/base_controller.py:11-266``),
   * ``MPCControllerHIP.run() -> (foot_wrench (B,2,6) float32, cost (B,))`` with the semantics of
     ``MPCControllerCusadi.run`` (``convex_mpc/mpc_controller_cusadi.py:43-205``).
-The whole step runs as four kernels on the caller's current HIP stream with no host
+The whole step runs as three kernels on the caller's current HIP stream with no host
 synchronisation: ``srbd_prepare_inputs`` (knot points, initial state, reference trajectory,
-contact schedule, I_world -- the ~40 small FP32 torch ops of the reference), ``qp_former``, the
+contact schedule, I_world -- the ~40 small FP32 torch ops of the reference), the fused former +
 PDIPM (cold start, ``cfg.pdipm_iterations`` Newton iterations in one launch; the reference runs
-4 calls x 5 iterations with host round trips) and ``srbd_u0_wrench``. Nothing of the step is
-computed in PyTorch; it only owns the buffers.
+a former call and 4 solver calls x 5 iterations with host round trips) and ``srbd_u0_wrench``;
+``GraphedMPCStep`` replays the three as one captured HIP graph. Nothing of the step is computed in
+PyTorch; it only owns the buffers.
 
 ``literal_layout=True`` (default) reproduces the reference GPU caller's flattening quirks
 (row-major R_body read column-major, row-major contact table read column-major, a 13-wide Q read
@@ -248,6 +249,51 @@ class MPCControllerHIP(BaseMPCController):
 
 # the reference's class name, for drop-in imports
 MPCControllerCusadi = MPCControllerHIP
+
+
+class GraphedMPCStep:
+    """The controller step captured once as a HIP graph and replayed: prepare -> fused former +
+    solver -> wrench (three kernels) become one graph launch, which matters when the batch is
+    small and launch overhead is a visible share of the step.
+
+    The graph records device pointers, so the state / command tensors handed to the controller must
+    keep their storage: update them in place (``copy_``) between replays. Everything else
+    (controller buffers, knot-point state) already lives in fixed tensors.
+    """
+
+    def __init__(self, controller: MPCControllerHIP, warmup: int = 1):
+        self.c = controller
+        self._keep: list = []
+        self._prep = self.c._prep_struct(self._keep)  # resolves every input pointer once
+        saved = [t.clone() for t in (controller.world_position_desired, controller.yaw_desired,
+                                     controller.first_run)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):  # first launches configure kernel attributes outside capture
+                self._launch()
+        torch.cuda.current_stream().wait_stream(s)
+        for dst, src in zip((controller.world_position_desired, controller.yaw_desired,
+                             controller.first_run), saved):
+            dst.copy_(src)  # the warm-up must not advance the knot-point state
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._launch()
+
+    def _launch(self) -> None:
+        c, N = self.c, self.c.horizon_length
+        L = _native.lib()
+        _native.check(L.srbd_prepare_inputs(N, c.num_envs, ctypes.byref(self._prep),
+                                            _native.ptr_array([t.data_ptr() for t in c.former_inputs]),
+                                            solver._stream_ptr()), "srbd_prepare_inputs")
+        out = solver.mpc_solve(c.former_inputs, N, c.cfg.pdipm_iterations, c.cfg.y0, c.buffers)
+        c.solution = out
+        _native.check(L.srbd_u0_wrench(N, c.num_envs, out[0].data_ptr(), self._prep.rotation_body,
+                                       c.foot_wrench.data_ptr(), solver._stream_ptr()), "srbd_u0_wrench")
+
+    def __call__(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        self.graph.replay()
+        return self.c.foot_wrench, self.c.cost
 
 
 def dense_scatter(values: torch.Tensor, inverse_index: torch.Tensor, shape: tuple[int, int],

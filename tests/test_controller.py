@@ -212,3 +212,24 @@ def test_controller_step_matches_oracle_pipeline():
     # test_gpu_parity.SOLVER_CASES); measured worst env 3.1e-5, others <= 3e-7. BASELINE bar: 1e-4.
     assert err.max() <= 1e-4, err.max()
     assert np.median(err) <= 1e-6, np.median(err)
+
+
+@pytest.mark.gpu
+def test_graphed_step_replays_the_controller_step():
+    """GraphedMPCStep: one captured graph launch per step, same wrench as run(), and replays pick
+    up state updated in place."""
+    from biped_pympc_amd.controller import GraphedMPCStep
+    N, B = 10, 64
+    st, cmd, ctrl, params, gait_args, table = random_robot(B, 31, N, gait=True)
+    c1 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    c2 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    g = GraphedMPCStep(c2)  # the warm-up launch leaves c2's knot-point state as it was
+    for step in range(3):
+        w1, _ = c1.run()
+        w2, _ = g()
+        torch.cuda.synchronize()
+        assert torch.equal(w1, w2), step
+        # move the robots: in-place updates are seen by the next replay
+        for c in (c1, c2):
+            c.state_estimate_data.root_position.add_(0.01)
+            c.state_estimate_data.foot_position.add_(0.01)
