@@ -315,8 +315,8 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) {
       const int q = lane + 64 * t;
       if (q < m) {
-        wd[t] = (1.0 / s[t]) * z[t] + kDelta;
-        di[t] = 1.0 / (1.0 + kDelta * wd[t]);
+        wd[t] = rcp3(s[t]) * z[t] + kDelta;  // correctly rounded reciprocals (rcp3), not IEEE division
+        di[t] = rcp3(1.0 + kDelta * wd[t]);
         VV[q] = di[t] * wd[t];  // Lambda, shared with the foot tasks
       }
     }
@@ -467,7 +467,7 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) {
       const int q = lane + 64 * t;
       if (q < m) {
-        const double si = 1.0 / s[t];
+        const double si = rcp3(s[t]);
         double r2 = -(si * (s[t] * z[t]));
         if (mode) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
         VV[q] = di[t] * (r2 + wd[t] * rs[t]);
@@ -506,8 +506,8 @@ struct RegCtx {
       } else {
         const int i = lane - 2 * N, b = 12 * i;
         const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
-        TV[nx + b + 6] = (kDelta * -RXu[b + 6] + SG[6] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
-        TV[nx + b + 9] = (kDelta * -RXu[b + 9] + SG[7] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
+        TV[nx + b + 6] = (kDelta * -RXu[b + 6] + SG[6] * r4a) * SG[8];  // SG[8] = 1 / (phi6 delta + e6^2)
+        TV[nx + b + 9] = (kDelta * -RXu[b + 9] + SG[7] * r4b) * SG[9];
         TV[nx + b + 8] = -RXu[b + 8] * SG[1];
         TV[nx + b + 11] = -RXu[b + 11] * SG[3];
       }
@@ -626,8 +626,8 @@ struct RegCtx {
         TV[b + 8] -= SG[1] * a8;
         TV[b + 11] -= SG[3] * a11;
         const double rho6 = -RXu[12 * i + 6] - a6, rho9 = -RXu[12 * i + 9] - a9;
-        DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
-        DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
+        DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) * SG[8];
+        DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) * SG[9];
       }
     }
     __syncthreads();
@@ -652,7 +652,7 @@ struct RegCtx {
       const int q = lane + 64 * t;
       if (q < m) {
         const bool c = dv[t] < 0.0;
-        const double a = -v[t] / dv[t];
+        const double a = -v[t] * rcp3(dv[t]);
         mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
       }
     }
@@ -804,6 +804,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     SG[5] = p9;
     SG[6] = e6;
     SG[7] = e9;
+    SG[8] = 1.0 / (p6 * kDelta + e6 * e6);
+    SG[9] = 1.0 / (p9 * kDelta + e9 * e9);
   }
   __syncthreads();
   if (lane < 24) {  // compact M and C (C = M diag(P / phi_x)); group 1's block is pi C^T pi^T
