@@ -75,11 +75,12 @@ struct SolverLayout {
 __device__ inline int sym_idx(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
 
 // Symmetric sweep of a small SPD matrix held in registers (packed lower) -> its inverse.
-template <int n>
+// kRcp: pivot reciprocals by rcp3 instead of IEEE division.
+template <int n, bool kRcp = false>
 __device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
 #pragma unroll
   for (int k = 0; k < n; ++k) {
-    const double id = 1.0 / a[k * (k + 1) / 2 + k];
+    const double id = kRcp ? rcp3(a[k * (k + 1) / 2 + k]) : 1.0 / a[k * (k + 1) / 2 + k];
     double col[n];
 #pragma unroll
     for (int i = 0; i < n; ++i) col[i] = a[sym_idx(i, k)];

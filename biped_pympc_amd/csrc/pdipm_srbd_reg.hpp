@@ -42,14 +42,6 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
-// 1/d: v_rcp_f64 (~2^-24 relative) refined by one cubically convergent step y (1 + e + e^2),
-// e = 1 - d y: three dependent FMAs instead of two Newton steps' four (critical path of a pivot)
-__device__ __forceinline__ double rcp3(double d) {
-  const double y = __builtin_amdgcn_rcp(d);
-  const double e = fma(-d, y, 1.0);
-  return fma(y, fma(e, e, e), y);
-}
-
 // ---- fused broadcast-FMA: v_fmac_f64_dpp row_newbcast:K (gfx90a+ 64-bit DPP on a VOP2 FMA) ----
 // acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
 // v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
@@ -340,7 +332,7 @@ struct RegCtx {
 #pragma unroll
           for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * gl[r] * gl[c];
       }
-      sweep_inverse<4>(a);
+      sweep_inverse<4, true>(a);
 #pragma unroll
       for (int e = 0; e < 10; ++e) {
         ph[e] = a[e];

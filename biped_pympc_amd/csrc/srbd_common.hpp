@@ -207,6 +207,15 @@ __device__ unsigned long long g_phase_cycles[16];
 #define PROF_FLUSH(ctx)
 #endif
 
+// 1/d: v_rcp_f64 (~2^-24 relative) refined by one cubically convergent step y (1 + e + e^2),
+// e = 1 - d y: three dependent FMAs instead of two Newton steps' four; correctly rounded on 4M
+// log-uniform samples (scripts/microbench_fp64.hip), about a third of an IEEE division's cost
+__device__ __forceinline__ double rcp3(double d) {
+  const double y = __builtin_amdgcn_rcp(d);
+  const double e = fma(-d, y, 1.0);
+  return fma(y, fma(e, e, e), y);
+}
+
 // ------------------------------------------------------------------ wave64 reductions ----
 __device__ inline double wave_sum(double v) {
 #pragma unroll
