@@ -340,11 +340,13 @@ struct RegCtx {
       }
     }
     __syncthreads();
-    for (int e = lane; e < 78 * N; e += 64) {  // S_ii = K + sum_f N_f Phi_f^-1 N_f^T
-      const int i = e / 78, l = e % 78;
-      const int rc = TRI[l];  // packed-lower position -> (row, col), table built once per kernel
-      const int r = rc & 15, c = rc >> 4;
-      double v = (i == 0 ? K0 : K1)[l];
+    // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in three divergence-free passes over the class-sorted
+    // entry table (TRI = c_tab.dvo): rows {3,4,5,9,10,11} of N hold one entry per foot (position
+    // r % 3), so an entry touching them needs 10 (one sparse index) or 4 (two) FMAs instead of 40
+    auto kval = [&](int i, int r, int c) { return (i == 0 ? K0 : K1)[r * (r + 1) / 2 + c]; };
+    for (int e = lane; e < 21 * N; e += 64) {  // dense x dense
+      const int i = e / 21, rc = TRI[e % 21], r = rc & 15, c = rc >> 4;
+      double v = kval(i, r, c);
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         const double* ph_ = PHs + 20 * i + 10 * f;
@@ -362,7 +364,31 @@ struct RegCtx {
           v += vr[a] * t;
         }
       }
-      DV[e] = v;
+      DV[78 * i + r * (r + 1) / 2 + c] = v;
+    }
+    for (int e = lane; e < 36 * N; e += 64) {  // sparse x dense
+      const int i = e / 36, rc = TRI[21 + e % 36], r = rc & 15, c = rc >> 4;
+      const bool rs = (r % 6) >= 3;
+      const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
+      double v = kval(i, r, c);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const double* ph_ = PHs + 20 * i + 10 * f;
+        double t = 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) t += ph_[sym_idx(as, b)] * Nd[dn * 12 + foot_colj(f, b)];
+        v += Nd[sp * 12 + foot_colj(f, as)] * t;
+      }
+      DV[78 * i + r * (r + 1) / 2 + c] = v;
+    }
+    for (int e = lane; e < 21 * N; e += 64) {  // sparse x sparse
+      const int i = e / 21, rc = TRI[57 + e % 21], r = rc & 15, c = rc >> 4;
+      const int ar = r % 3, ac = c % 3;
+      double v = kval(i, r, c);
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+        v += Nd[r * 12 + foot_colj(f, ar)] * PHs[20 * i + 10 * f + sym_idx(ar, ac)] * Nd[c * 12 + foot_colj(f, ac)];
+      DV[78 * i + r * (r + 1) / 2 + c] = v;
     }
     __syncthreads();
     PROF_ADD(1);
@@ -780,11 +806,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
   }
   // ---- per-QP constants ----
-  for (int l = lane; l < 78; l += 64) {  // packed-lower index -> (row | col << 4)
-    int r, c;
-    tri_rc(l, r, c);
-    reinterpret_cast<uint8_t*>(smem + Lo::TRI)[l] = (uint8_t)(r | (c << 4));
-  }
+  for (int l = lane; l < 78; l += 64) reinterpret_cast<uint8_t*>(smem + Lo::TRI)[l] = c_tab.dvo[l];
   if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
   if (lane == 0) {
     const double p6 = Hu[6] + kBeta, p9 = Hu[9] + kBeta;

@@ -48,6 +48,10 @@ struct Tables {
   // row -1 = the +I entry of an x column, row 12/13 = the x-moment entries e6/e9 of a u block.
   int8_t xb_r[36], xb_j[36];
   int8_t ub_r[86], ub_j[86];
+  // Packed-lower 12x12 entries (row | col << 4, row >= col) sorted for the S_ii build: rows/cols
+  // {0,1,2,6,7,8} meet every foot column of N ("dense"), rows {3,4,5,9,10,11} exactly one per foot
+  // (position r % 3). Order: 21 dense-dense, 36 sparse-dense, 21 sparse-sparse.
+  uint8_t dvo[78];
   // Foot blocks of Phi_u: u columns {0,1,2,7} (left) and {3,4,5,10} (right).
   int8_t foot_col[2][4];
   // column -> (foot, position) or -1 for the four decoupled columns {6,8,9,11}
@@ -142,6 +146,15 @@ constexpr Tables make_tables() {
     t.gr_off[k][t.gr_n[k]] = (int8_t)q;
     t.gr_col[k][t.gr_n[k]] = t.gcol[q];
     t.gr_n[k]++;
+  }
+  {
+    int o = 0;
+    for (int cls = 0; cls < 3; ++cls)
+      for (int r = 0; r < 12; ++r)
+        for (int c = 0; c <= r; ++c) {
+          const int sparse = (r % 6 >= 3) + (c % 6 >= 3);
+          if (sparse == cls) t.dvo[o++] = (uint8_t)(r | (c << 4));
+        }
   }
   const int8_t fl[4] = {0, 1, 2, 7}, fr[4] = {3, 4, 5, 10};
   for (int q = 0; q < 4; ++q) {
