@@ -756,7 +756,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #pragma unroll
     for (int t = 0; t < SI; ++t)
       if (lane + 64 * t < m) dw[lane + 64 * t] = former_d(lane + 64 * t, N, P[2], P[12], mu);
-    __threadfence();
+    // each entry is re-read only by the lane that wrote it: workgroup scope orders that (a device-
+    // scope release would write back L2)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     C.fg = fw;
     C.bg = bw;
     C.hg = dw;
