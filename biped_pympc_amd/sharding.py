@@ -53,6 +53,10 @@ class ShardedMPC:
             self._recv = torch.empty((self.world * self.slot, 12), dtype=torch.float64, device=self.device)
             keep = [r * self.slot + i for r, (l, h) in enumerate(self.sizes) for i in range(h - l)]
             self._keep = torch.tensor(keep, dtype=torch.int64, device=self.device)
+        # step_async: double-buffered send / receive so a gather in flight never reads or writes a
+        # buffer the next step is using
+        self._abuf = None
+        self._aidx = 0
 
     @property
     def local_envs(self) -> int:
@@ -76,6 +80,35 @@ class ShardedMPC:
         self.x_local = self._solve(local_inputs)
         self.gather_u0(self.x_local[:, 12 * self.N:12 * self.N + 12])
         return self.u0_all
+
+    def step_async(self, local_inputs: Sequence[torch.Tensor]) -> "PendingGather":
+        """Like ``step`` but the u0 gather is left running on the collective's own stream (RCCL),
+        so it overlaps the next step's solve; ``.wait()`` on the returned handle yields u0 of every
+        env. Two steps' gathers may be in flight; a handle must be waited before the step after
+        next reuses its buffers (``PendingGather.wait`` is idempotent)."""
+        if local_inputs[0].shape[0] != self.local_envs:
+            raise ValueError(f"rank {self.rank}: expected {self.local_envs} envs, got {local_inputs[0].shape[0]}")
+        self.x_local = self._solve(local_inputs)
+        u0 = self.x_local[:, 12 * self.N:12 * self.N + 12]
+        if self.world == 1:
+            return PendingGather(u0, None, None)
+        if self._abuf is None:
+            mk = lambda *sh: torch.zeros(sh, dtype=torch.float64, device=self.device)  # noqa: E731
+            self._abuf = [(mk(self.slot, 12), mk(self.world * self.slot, 12)) for _ in range(2)]
+            self._apending = [None, None]
+        k = self._aidx
+        self._aidx ^= 1
+        if self._apending[k] is not None:  # the gather that used this buffer pair two steps ago
+            self._apending[k].wait()
+        send, recv = self._abuf[k]
+        send[:self.local_envs].copy_(u0)  # on the compute stream, before the collective is enqueued
+        if dist.get_backend(self.group) == "nccl":
+            work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+        else:
+            work = dist.all_gather(list(recv.split(self.slot)), send, group=self.group, async_op=True)
+        keep = self._keep if self._ragged else None
+        self._apending[k] = PendingGather(recv, work, keep)
+        return self._apending[k]
 
     @property
     def buffers(self):
@@ -101,3 +134,17 @@ class ShardedMPC:
             dist.all_gather(list(self._recv.split(self.slot)), self._send, group=self.group)
         torch.index_select(self._recv, 0, self._keep, out=self.u0_all)
         return self.u0_all
+
+
+class PendingGather:
+    """Handle of an in-flight u0 gather (``ShardedMPC.step_async``)."""
+
+    def __init__(self, buf: torch.Tensor, work, keep: torch.Tensor | None):
+        self._buf, self._work, self._keep, self._out = buf, work, keep, None
+
+    def wait(self) -> torch.Tensor:
+        if self._out is None:
+            if self._work is not None:
+                self._work.wait()  # the current stream now waits for the collective
+            self._out = self._buf if self._keep is None else self._buf.index_select(0, self._keep)
+        return self._out

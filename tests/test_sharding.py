@@ -56,8 +56,10 @@ def _rank_main(rank, world, port, total, out_path):
         sh = ShardedMPC(N, K, total, device="cpu", solve_fn=_oracle_solve)
         u0 = sh.step(sh.local_slice(glob)).clone()
         u0b = sh.step(sh.local_slice(glob)).clone()  # buffers reused across steps
+        hs = [sh.step_async(sh.local_slice(glob)) for _ in range(3)]  # gathers left in flight
+        u0c = [h.wait().clone() for h in hs]
         if rank == 0:
-            np.save(out_path, np.stack([u0.numpy(), u0b.numpy()]))
+            np.save(out_path, np.stack([u0.numpy(), u0b.numpy()] + [u.numpy() for u in u0c]))
     finally:
         dist.destroy_process_group()
 
@@ -75,8 +77,9 @@ def test_gloo_world2_gather_equals_single_process(tmp_path, total):
     got = np.load(out)
     wl = make_workload(total, N, seed=2024, random_gait=True)
     ref = _oracle_solve([torch.from_numpy(a) for a in wl.inputs]).numpy()[:, 12 * N:12 * N + 12]
-    assert got.shape == (2, total, 12)
-    assert np.array_equal(got[0], ref) and np.array_equal(got[1], ref)
+    assert got.shape == (5, total, 12)
+    for k in range(5):
+        assert np.array_equal(got[k], ref), k
 
 
 def test_single_process_path_without_process_group():
