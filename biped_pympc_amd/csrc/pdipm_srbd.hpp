@@ -56,14 +56,6 @@ __device__ __forceinline__ double bc16(double v, int k) {
   }
 }
 
-// 1/d: v_rcp_f64 refined by two Newton steps (a correctly-rounded division costs ~10 dependent
-// instructions on the critical path of the sweep)
-__device__ __forceinline__ double rcp_nr(double d) {
-  double y = __builtin_amdgcn_rcp(d);
-  y = fma(y, fma(-d, y, 1.0), y);
-  return fma(y, fma(-d, y, 1.0), y);
-}
-
 // LDS hand-off between lanes of ONE wavefront: DS ops of a wave complete in order, so only the
 // compiler must be kept from reordering; the wait also drains outstanding LDS ops.
 __device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -71,27 +63,84 @@ __device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcn
 // (j + 6) mod 12: swaps the (euler, position) and (omega, velocity) halves of the SRBD state
 __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 
-// In-place symmetric sweep of a 12x12 SPD block held one row per lane (row r in lane r of a
-// 16-lane DPP row; lanes 12..15 shadow row 11): afterwards Sr = -(row r of the inverse).
-// Pivot k: a_rj <- a_rj - a_rk a_kj / d (r != k), a_kj <- a_kj / d, a_rk <- a_rk / d,
-// a_kk <- -1/d, written as fma(coef, a_kj, sc * a_rj) with (coef, sc) = (-a_rk/d, 1) off the pivot
-// row and (1/d, 0) on it; the pivot row a_k* is broadcast with v_mov_b64_dpp row_newbcast.
-__device__ __forceinline__ void sweep12(double (&Sr)[12], int r) {
+// ---- fused broadcast-FMA: v_fmac_f64_dpp row_newbcast:K (gfx90a+ 64-bit DPP on a VOP2 FMA) ----
+// acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
+// v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
+// they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
+// entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
+// block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
+#define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
+
+// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for all 12 j (j == K included; the
+// caller overwrites S[K] afterwards)
+#define SRBD_PIVOT_BLOCK(K)                                                                          \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%0", "%12", K) SRBD_FMAC_BC("%1", "%1", "%12", K)              \
+          SRBD_FMAC_BC("%2", "%2", "%12", K) SRBD_FMAC_BC("%3", "%3", "%12", K)                       \
+              SRBD_FMAC_BC("%4", "%4", "%12", K) SRBD_FMAC_BC("%5", "%5", "%12", K)                   \
+                  SRBD_FMAC_BC("%6", "%6", "%12", K) SRBD_FMAC_BC("%7", "%7", "%12", K)               \
+                      SRBD_FMAC_BC("%8", "%8", "%12", K) SRBD_FMAC_BC("%9", "%9", "%12", K)           \
+                          SRBD_FMAC_BC("%10", "%10", "%12", K) SRBD_FMAC_BC("%11", "%11", "%12", K) "s_nop 1\n" \
+      : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]), \
+        "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11])                                              \
+      : "v"(coef))
+__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k) {
+  switch (k) {
+    case 0: SRBD_PIVOT_BLOCK(0); break;
+    case 1: SRBD_PIVOT_BLOCK(1); break;
+    case 2: SRBD_PIVOT_BLOCK(2); break;
+    case 3: SRBD_PIVOT_BLOCK(3); break;
+    case 4: SRBD_PIVOT_BLOCK(4); break;
+    case 5: SRBD_PIVOT_BLOCK(5); break;
+    case 6: SRBD_PIVOT_BLOCK(6); break;
+    case 7: SRBD_PIVOT_BLOCK(7); break;
+    case 8: SRBD_PIVOT_BLOCK(8); break;
+    case 9: SRBD_PIVOT_BLOCK(9); break;
+    case 10: SRBD_PIVOT_BLOCK(10); break;
+    default: SRBD_PIVOT_BLOCK(11); break;
+  }
+}
+
+// sum_j c[j] * v(lane j) over the 12 rows of a 16-lane DPP row (three interleaved accumulators)
+__device__ __forceinline__ double dot_bc12(const double (&c)[12], double v) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%3", "%4", 0) SRBD_FMAC_BC("%1", "%3", "%5", 1) SRBD_FMAC_BC("%2", "%3", "%6", 2)
+      SRBD_FMAC_BC("%0", "%3", "%7", 3) SRBD_FMAC_BC("%1", "%3", "%8", 4) SRBD_FMAC_BC("%2", "%3", "%9", 5)
+      SRBD_FMAC_BC("%0", "%3", "%10", 6) SRBD_FMAC_BC("%1", "%3", "%11", 7) SRBD_FMAC_BC("%2", "%3", "%12", 8)
+      SRBD_FMAC_BC("%0", "%3", "%13", 9) SRBD_FMAC_BC("%1", "%3", "%14", 10) SRBD_FMAC_BC("%2", "%3", "%15", 11)
+      "s_nop 1\n"
+      : "+v"(a0), "+v"(a1), "+v"(a2)
+      : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
+        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));
+  return (a0 + a1) + a2;
+}
+
+// Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r in lane r of a 16-lane
+// DPP row; lanes 12..15 shadow row 11), by Gauss-Jordan pivoting on the diagonal. The
+// pivot row is not rescaled in place (a plain sweep would multiply every element of every row by
+// a select to special-case it): every lane keeps its row unscaled together with a scale
+// factor (1/pivot once the row has been the pivot) that is applied once at the end, so each pivot
+// costs one fused broadcast-FMA per element and lane (pivot_update; no per-element select).
+//   pivot k (pk = row k, broadcast by row_newbcast inside the FMAs, id = 1/pk[k] by rcp3):
+//     lane r != k: a_rj <- a_rj - a_rk id pk_j  (j != k),  a_rk <- a_rk id
+//     lane k     : row unchanged except a_kk <- -1, scale <- id
+// On exit Dr[j] = (A^-1)_rj.
+__device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (&Dr)[12]) {
+  double sc = 1.0;
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
-    double pk[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) pk[j] = bc16(Sr[j], k);
-    const double id = rcp_nr(pk[k]);
+    const double id = rcp3(bc16(Sr[k], k));
     const bool piv = (r == k);
     const double ark = Sr[k];
-    const double coef = piv ? id : -ark * id;
-    const double sc = piv ? 0.0 : 1.0;
-#pragma unroll
-    for (int j = 0; j < 12; ++j)
-      if (j != k) Sr[j] = fma(coef, pk[j], sc * Sr[j]);
-    Sr[k] = piv ? -id : ark * id;
+    const double coef = piv ? 0.0 : -ark * id;
+    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef (pk = row k, fused broadcast)
+    Sr[k] = piv ? -1.0 : ark * id;
+    sc = piv ? id : sc;
   }
+  // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
+  const double nsc = -sc;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) Dr[j] = Sr[j] * nsc;
 }
 
 // packed-lower index -> (row, col), computed without loops
@@ -326,9 +375,7 @@ struct FastCtx {
             }
           }
           if (act && !(mstep && g == 1)) {
-            sweep12(Sr, r);
-#pragma unroll
-            for (int c = 0; c < 12; ++c) Dr[c] = -Sr[c];
+            inverse_rows12(Sr, r, Dr);
             if (own) {
               double* Di = DV + 78 * i;
 #pragma unroll

@@ -42,71 +42,6 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
-// ---- fused broadcast-FMA: v_fmac_f64_dpp row_newbcast:K (gfx90a+ 64-bit DPP on a VOP2 FMA) ----
-// acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
-// v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
-// they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
-// entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
-// block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
-#define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
-
-// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for all 12 j (j == K included; the
-// caller overwrites S[K] afterwards)
-#define SRBD_PIVOT_BLOCK(K)                                                                          \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%0", "%12", K) SRBD_FMAC_BC("%1", "%1", "%12", K)              \
-          SRBD_FMAC_BC("%2", "%2", "%12", K) SRBD_FMAC_BC("%3", "%3", "%12", K)                       \
-              SRBD_FMAC_BC("%4", "%4", "%12", K) SRBD_FMAC_BC("%5", "%5", "%12", K)                   \
-                  SRBD_FMAC_BC("%6", "%6", "%12", K) SRBD_FMAC_BC("%7", "%7", "%12", K)               \
-                      SRBD_FMAC_BC("%8", "%8", "%12", K) SRBD_FMAC_BC("%9", "%9", "%12", K)           \
-                          SRBD_FMAC_BC("%10", "%10", "%12", K) SRBD_FMAC_BC("%11", "%11", "%12", K) "s_nop 1\n" \
-      : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4), "+v"(s5), "+v"(s6), "+v"(s7), "+v"(s8),      \
-        "+v"(s9), "+v"(s10), "+v"(s11)                                                                \
-      : "v"(coef))
-// S[j] += S[j](lane k) * coef for every j except `skip`, whose operand slot takes `junk`
-__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k, int skip, double& junk) {
-  double& s0 = skip == 0 ? junk : S[0];
-  double& s1 = skip == 1 ? junk : S[1];
-  double& s2 = skip == 2 ? junk : S[2];
-  double& s3 = skip == 3 ? junk : S[3];
-  double& s4 = skip == 4 ? junk : S[4];
-  double& s5 = skip == 5 ? junk : S[5];
-  double& s6 = skip == 6 ? junk : S[6];
-  double& s7 = skip == 7 ? junk : S[7];
-  double& s8 = skip == 8 ? junk : S[8];
-  double& s9 = skip == 9 ? junk : S[9];
-  double& s10 = skip == 10 ? junk : S[10];
-  double& s11 = skip == 11 ? junk : S[11];
-  switch (k) {
-    case 0: SRBD_PIVOT_BLOCK(0); break;
-    case 1: SRBD_PIVOT_BLOCK(1); break;
-    case 2: SRBD_PIVOT_BLOCK(2); break;
-    case 3: SRBD_PIVOT_BLOCK(3); break;
-    case 4: SRBD_PIVOT_BLOCK(4); break;
-    case 5: SRBD_PIVOT_BLOCK(5); break;
-    case 6: SRBD_PIVOT_BLOCK(6); break;
-    case 7: SRBD_PIVOT_BLOCK(7); break;
-    case 8: SRBD_PIVOT_BLOCK(8); break;
-    case 9: SRBD_PIVOT_BLOCK(9); break;
-    case 10: SRBD_PIVOT_BLOCK(10); break;
-    default: SRBD_PIVOT_BLOCK(11); break;
-  }
-}
-
-// sum_j c[j] * v(lane j) over the 12 rows of a 16-lane DPP row (three interleaved accumulators)
-__device__ __forceinline__ double dot_bc12(const double (&c)[12], double v) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  asm("s_nop 1\n"
-      SRBD_FMAC_BC("%0", "%3", "%4", 0) SRBD_FMAC_BC("%1", "%3", "%5", 1) SRBD_FMAC_BC("%2", "%3", "%6", 2)
-      SRBD_FMAC_BC("%0", "%3", "%7", 3) SRBD_FMAC_BC("%1", "%3", "%8", 4) SRBD_FMAC_BC("%2", "%3", "%9", 5)
-      SRBD_FMAC_BC("%0", "%3", "%10", 6) SRBD_FMAC_BC("%1", "%3", "%11", 7) SRBD_FMAC_BC("%2", "%3", "%12", 8)
-      SRBD_FMAC_BC("%0", "%3", "%13", 9) SRBD_FMAC_BC("%1", "%3", "%14", 10) SRBD_FMAC_BC("%2", "%3", "%15", 11)
-      "s_nop 1\n"
-      : "+v"(a0), "+v"(a1), "+v"(a2)
-      : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
-        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));
-  return (a0 + a1) + a2;
-}
-
 // acc[i] += v[i](lane 6) c6 + v[i](lane 7) c7 + v[i](lane 8) c8 for 4 elements (the rows 6..8 term
 // of the Schur update X = C V)
 __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x2, double& x3, double v0,
@@ -120,33 +55,6 @@ __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x
       "s_nop 1\n"
       : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
       : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8));
-}
-
-// Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r in lane r of a 16-lane
-// DPP row; lanes 12..15 shadow row 11), by Gauss-Jordan pivoting on the diagonal. Unlike sweep12 the
-// pivot row is not rescaled in place: every lane keeps its row unscaled together with a scale
-// factor (1/pivot once the row has been the pivot) that is applied once at the end, so each pivot
-// costs 11 FMAs per lane (no per-element select or multiply for the pivot lane).
-//   pivot k (pk = row k, broadcast with v_mov_b64_dpp row_newbcast, id = 1/pk[k]):
-//     lane r != k: a_rj <- a_rj - a_rk id pk_j  (j != k),  a_rk <- a_rk id
-//     lane k     : row unchanged except a_kk <- -1, scale <- id
-// On exit Dr[j] = (A^-1)_rj.
-__device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (&Dr)[12]) {
-  double sc = 1.0, junk = 0.0;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) {
-    const double id = rcp3(bc16(Sr[k], k));
-    const bool piv = (r == k);
-    const double ark = Sr[k];
-    const double coef = piv ? 0.0 : -ark * id;
-    pivot_update(Sr, coef, k, -1, junk);  // Sr[j] += pk[j] * coef (pk = row k, fused broadcast)
-    Sr[k] = piv ? -1.0 : ark * id;
-    sc = piv ? id : sc;
-  }
-  // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
-  const double nsc = -sc;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) Dr[j] = Sr[j] * nsc;
 }
 
 // element (c, b) of a compact M / C block (c or b runtime)
