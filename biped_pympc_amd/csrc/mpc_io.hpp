@@ -57,83 +57,82 @@ __device__ __forceinline__ float dot3f(float m0, float m1, float m2, float v0, f
   return (m0 * v0 + m1 * v1) + m2 * v2;
 }
 
+// One wave per env (4 per 256-thread block): the per-env scalars are wave-uniform, and the 64 lanes
+// write each output row contiguously (coalesced); lane 0 alone updates the knot-point state.
 __global__ __launch_bounds__(256) void prepare_inputs_kernel(PrepArgs a) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= a.batch) return;
   const int N = a.N;
   double* const* o = a.out;
   const float* rp = a.root_position + 3 * e;
   const float* eu = a.root_euler + 3 * e;
-  // compute_knot_points (base_controller.py:166-176)
-  float w0 = a.wpd[3 * e], w1 = a.wpd[3 * e + 1], w2 = a.wpd[3 * e + 2], yaw = a.yaw_des[e];
-  if (a.first_run[e]) {
-    w0 = rp[0];
-    w1 = rp[1];
-    w2 = rp[2];
-    yaw = eu[2];
-    a.first_run[e] = 0;
-  }
-  // set_initial_state (:201-211) -> x0 (input 0)
-  double* x0 = o[0] + (size_t)e * 12;
-  for (int j = 0; j < 3; ++j) {
-    x0[j] = eu[j];
-    x0[3 + j] = rp[j];
-    x0[6 + j] = a.ang_vel_w[3 * e + j];
-    x0[9 + j] = a.vel_w[3 * e + j];
-  }
+  // compute_knot_points (base_controller.py:166-176); every lane reads first_run before lane 0
+  // clears it (one instruction stream)
+  const bool first = a.first_run[e] != 0;
+  float w0 = first ? rp[0] : a.wpd[3 * e], w1 = first ? rp[1] : a.wpd[3 * e + 1];
+  float yaw = first ? eu[2] : a.yaw_des[e];
   // compute_reference_trajectory (:213-257)
   const float* vb = a.des_vel_b + 3 * e;
   const float wz = a.des_angvel_b[3 * e + 2], h = a.des_height[e], dt = a.dt_mpc[e];
   w0 = fa(w0, fm(a.step_dt, vb[0]));
   w1 = fa(w1, fm(a.step_dt, vb[1]));
-  w2 = h;
   yaw = fa(yaw, fm(a.step_dt, wz));
   const bool stationary = fabsf(vb[0]) < 1e-2f;
   const float* Rm = a.rotation_body + 9 * e;
   const float vw0 = dot3f(Rm[0], Rm[1], Rm[2], vb[0], vb[1], vb[2]);
   const float vw1 = dot3f(Rm[3], Rm[4], Rm[5], vb[0], vb[1], vb[2]);
   const float px = stationary ? w0 : rp[0], py = stationary ? w1 : rp[1];
+  if (lane == 0) {
+    a.wpd[3 * e] = w0;
+    a.wpd[3 * e + 1] = w1;
+    a.wpd[3 * e + 2] = h;
+    a.yaw_des[e] = yaw;
+    a.first_run[e] = 0;
+    o[4][e] = (double)dt;
+    o[5][e] = a.mass;
+    o[6][e] = a.mu;
+  }
+  // x_ref (input 3) and the linearisation points x, u = ones (mpc_controller_cusadi.py:55-57)
   double* xr = o[3] + (size_t)e * 12 * N;
-  for (int k = 0; k < N; ++k) {
+  for (int q = lane; q < 12 * N; q += 64) {
+    const int k = q / 12, j = q % 12;
     const float t = fm(dt, (float)k);
-    double* r = xr + 12 * k;
-    r[0] = 0.0;
-    r[1] = 0.0;
-    r[2] = fa(yaw, fm(wz, t));
-    r[3] = fa(px, fm(vw0, t));
-    r[4] = fa(py, fm(vw1, t));
-    r[5] = h;
-    r[6] = 0.0;
-    r[7] = 0.0;
-    r[8] = wz;
-    r[9] = vw0;
-    r[10] = vw1;
-    r[11] = 0.0;
+    float v;
+    switch (j) {
+      case 2: v = fa(yaw, fm(wz, t)); break;
+      case 3: v = fa(px, fm(vw0, t)); break;
+      case 4: v = fa(py, fm(vw1, t)); break;
+      case 5: v = h; break;
+      case 8: v = wz; break;
+      case 9: v = vw0; break;
+      case 10: v = vw1; break;
+      default: v = 0.0f; break;
+    }
+    xr[q] = v;
+    o[1][(size_t)e * 12 * N + q] = 1.0;
+    o[2][(size_t)e * 12 * N + q] = 1.0;
   }
-  a.wpd[3 * e] = w0;
-  a.wpd[3 * e + 1] = w1;
-  a.wpd[3 * e + 2] = w2;
-  a.yaw_des[e] = yaw;
-  // linearisation points x, u = ones (mpc_controller_cusadi.py:55-56)
-  for (int j = 0; j < 12 * N; ++j) {
-    o[1][(size_t)e * 12 * N + j] = 1.0;
-    o[2][(size_t)e * 12 * N + j] = 1.0;
-  }
-  o[4][e] = (double)dt;
-  o[5][e] = a.mass;
-  o[6][e] = a.mu;
-  // R_body (:58): row-major flattening (literal; CasADi decodes it column-major) or column-major
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) o[7][(size_t)e * 9 + (a.literal ? 3 * i + j : 3 * j + i)] = Rm[3 * i + j];
-  // I_world = R I_body R^T as two FP32 batched matmuls (:59-61)
-  float T[9];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j)
-      T[3 * i + j] = dot3f(Rm[3 * i], Rm[3 * i + 1], Rm[3 * i + 2], a.I_body[j], a.I_body[3 + j], a.I_body[6 + j]);
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j)
-      o[8][(size_t)e * 9 + 3 * i + j] = dot3f(T[3 * i], T[3 * i + 1], T[3 * i + 2], Rm[3 * j], Rm[3 * j + 1], Rm[3 * j + 2]);
-  for (int j = 0; j < 3; ++j) {
+  if (lane < 12) {  // set_initial_state (:201-211) -> x0; Q, R (:70-71)
+    const int g = lane / 3, j = lane % 3;
+    const float* src = g == 0 ? eu : g == 1 ? rp : g == 2 ? a.ang_vel_w + 3 * e : a.vel_w + 3 * e;
+    o[0][(size_t)e * 12 + lane] = src[j];
+    // the caller hands a (B, 13) Q to an input read with stride 12, so env e sees
+    // Q[(12 e + j) mod 13]; written here into a well-formed (B, 12)
+    const int qi = (a.literal && a.q_len == 13) ? (int)(((long long)12 * e + lane) % 13) : lane;
+    o[13][(size_t)e * 12 + lane] = a.Q[qi];
+    o[14][(size_t)e * 12 + lane] = a.R[lane];
+  } else if (lane < 21) {  // R_body (:58): row-major flattening (literal) or column-major; I_world
+    const int l = lane - 12, i = l / 3, j = l % 3;
+    o[7][(size_t)e * 9 + (a.literal ? 3 * i + j : 3 * j + i)] = Rm[3 * i + j];
+    // I_world = R I_body R^T as two FP32 batched matmuls (:59-61): row i of T = R I_body first
+    float T[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      T[k] = dot3f(Rm[3 * i], Rm[3 * i + 1], Rm[3 * i + 2], a.I_body[k], a.I_body[3 + k], a.I_body[6 + k]);
+    o[8][(size_t)e * 9 + 3 * i + j] = dot3f(T[0], T[1], T[2], Rm[3 * j], Rm[3 * j + 1], Rm[3 * j + 2]);
+  } else if (lane < 24) {
+    const int j = lane - 21;
     o[9][(size_t)e * 3 + j] = rp[j];
     o[10][(size_t)e * 3 + j] = a.foot_position[6 * e + j];
     o[11][(size_t)e * 3 + j] = a.foot_position[6 * e + 3 + j];
@@ -143,36 +142,28 @@ __global__ __launch_bounds__(256) void prepare_inputs_kernel(PrepArgs a) {
   // contact schedule: GaitGenerator.mpc_gait (gait_generator.py:216-252) or the given table;
   // flattened (N,2) row-major as the caller does (:65; literal) or column-major (corrected)
   double* ct = o[12] + (size_t)e * 2 * N;
-  if (a.gait_phase) {
-    const int s0 = a.ssp[2 * e], s1 = a.ssp[2 * e + 1], d0 = a.dsp[2 * e], d1 = a.dsp[2 * e + 1];
-    const int cyc = s0 + s1 + d0 + d1;
-    const int g = (int)fm(a.gait_phase[e], (float)cyc);  // (phase * cycle).int(): truncation
-    for (int k = 0; k < N; ++k) {
+  for (int k = lane; k < N; k += 64) {
+    double cl, cr;
+    if (a.gait_phase) {
+      const int s0 = a.ssp[2 * e], s1 = a.ssp[2 * e + 1], d0 = a.dsp[2 * e], d1 = a.dsp[2 * e + 1];
+      const int cyc = s0 + s1 + d0 + d1;
       if (cyc <= 0) {  // degenerate durations (torch would fault on % 0): double support
-        ct[a.literal ? 2 * k : k] = 1.0;
-        ct[a.literal ? 2 * k + 1 : N + k] = 1.0;
-        continue;
+        cl = cr = 1.0;
+      } else {
+        const int g = (int)fm(a.gait_phase[e], (float)cyc);  // (phase * cycle).int(): truncation
+        int st = (g + k) % cyc;
+        if (st < 0) st += cyc;  // torch remainder takes the divisor's sign
+        const bool p1 = st < s1, p2 = st >= s1 && st < s1 + d0, p3 = st >= s1 + d0 && st < s1 + d0 + s0;
+        const bool fin = !(p1 || p2 || p3);
+        cl = (p1 || p2 || fin) ? 1.0 : 0.0;
+        cr = (p2 || p3 || fin) ? 1.0 : 0.0;
       }
-      int st = (g + k) % cyc;
-      if (st < 0) st += cyc;  // torch remainder takes the divisor's sign
-      const bool p1 = st < s1, p2 = st >= s1 && st < s1 + d0, p3 = st >= s1 + d0 && st < s1 + d0 + s0;
-      const bool fin = !(p1 || p2 || p3);
-      const double cl = (p1 || p2 || fin) ? 1.0 : 0.0, cr = (p2 || p3 || fin) ? 1.0 : 0.0;
-      ct[a.literal ? 2 * k : k] = cl;
-      ct[a.literal ? 2 * k + 1 : N + k] = cr;
+    } else {
+      cl = a.contact_table[(size_t)e * 2 * N + 2 * k];
+      cr = a.contact_table[(size_t)e * 2 * N + 2 * k + 1];
     }
-  } else {
-    for (int k = 0; k < N; ++k) {
-      ct[a.literal ? 2 * k : k] = a.contact_table[(size_t)e * 2 * N + 2 * k];
-      ct[a.literal ? 2 * k + 1 : N + k] = a.contact_table[(size_t)e * 2 * N + 2 * k + 1];
-    }
-  }
-  // Q, R (:70-71). The caller hands a (B, 13) Q to an input read with stride 12, so env e sees
-  // Q[(12 e + j) mod 13]; that is written here into a well-formed (B, 12).
-  for (int j = 0; j < 12; ++j) {
-    const int qi = (a.literal && a.q_len == 13) ? (int)(((long long)12 * e + j) % 13) : j;
-    o[13][(size_t)e * 12 + j] = a.Q[qi];
-    o[14][(size_t)e * 12 + j] = a.R[j];
+    ct[a.literal ? 2 * k : k] = cl;
+    ct[a.literal ? 2 * k + 1 : N + k] = cr;
   }
 }
 
@@ -197,15 +188,30 @@ __global__ __launch_bounds__(256) void u0_wrench_kernel(int N, int batch, const 
   }
 }
 
-// dense (B, rc) from CCS nonzeros (B, nnz) through inv[rc] (nonzero index or -1)
+// dense (B, rc) from CCS nonzeros (B, nnz) through inv[rc] (nonzero index or -1); each thread
+// writes two consecutive entries with one 16-byte store when rc is even (every env's row is then
+// 16-byte aligned), one 8-byte store otherwise
 __global__ __launch_bounds__(256) void dense_scatter_kernel(int rc, int nnz, int batch, const int32_t* __restrict__ inv,
                                                             const double* __restrict__ vals,
                                                             double* __restrict__ dense) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = blockIdx.y;
-  if (idx >= rc || e >= batch) return;
-  const int k = inv[idx];
-  dense[(size_t)e * rc + idx] = k >= 0 ? vals[(size_t)e * nnz + k] : 0.0;
+  if (e >= batch) return;
+  const double* v = vals + (size_t)e * nnz;
+  double* out = dense + (size_t)e * rc;
+  if ((rc & 1) == 0) {
+    const int i0 = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (i0 >= rc) return;
+    const int2 k = *reinterpret_cast<const int2*>(inv + i0);
+    double2 r;
+    r.x = k.x >= 0 ? v[k.x] : 0.0;
+    r.y = k.y >= 0 ? v[k.y] : 0.0;
+    *reinterpret_cast<double2*>(out + i0) = r;
+  } else {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rc; i += gridDim.x * blockDim.x) {
+      const int k = inv[i];
+      out[i] = k >= 0 ? v[k] : 0.0;
+    }
+  }
 }
 
 }  // namespace srbd

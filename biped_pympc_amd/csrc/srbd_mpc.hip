@@ -404,7 +404,7 @@ int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* p, double* 
   }
   a.N = horizon;
   a.batch = batch;
-  hipLaunchKernelGGL(srbd::prepare_inputs_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(srbd::prepare_inputs_kernel, dim3((batch + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "prepare_inputs_kernel launch");
 }
@@ -426,7 +426,7 @@ int srbd_dense_scatter(int batch, int nnz, int rc, const int* inverse_index, con
       (batch > 0 && rc > 0 && (!inverse_index || !dense || (nnz > 0 && !values))))
     return set_error(kErrInvalid, "srbd_dense_scatter: bad arguments (batch <= 65535 per call)");
   if (batch == 0 || rc == 0) return 0;
-  hipLaunchKernelGGL(srbd::dense_scatter_kernel, dim3((rc + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, rc,
+  hipLaunchKernelGGL(srbd::dense_scatter_kernel, dim3((rc + 511) / 512, batch), dim3(256), 0, (hipStream_t)stream, rc,
                      nnz, batch, (const int32_t*)inverse_index, values, dense);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "dense_scatter_kernel launch");
