@@ -69,6 +69,9 @@ def lib() -> ctypes.CDLL:
     L.srbd_prepare_inputs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(MPCPrep), P, ctypes.c_void_p]
     L.srbd_u0_wrench.restype = ctypes.c_int
     L.srbd_u0_wrench.argtypes = [ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
+    L.srbd_u0_wrench_torque.restype = ctypes.c_int
+    L.srbd_u0_wrench_torque.argtypes = [ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int, _c_dp,
+                                        _c_dp, _c_dp, ctypes.c_void_p]
     L.srbd_dense_scatter.restype = ctypes.c_int
     L.srbd_dense_scatter.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp,
                                      ctypes.c_void_p]

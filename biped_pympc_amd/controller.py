@@ -175,6 +175,7 @@ class MPCControllerHIP(BaseMPCController):
         self.buffers = solver.MPCSolveBuffers.allocate(N, B, dev)
         self.foot_wrench = torch.empty((B, 2, 6), dtype=torch.float32, device=dev)
         self.cost = torch.zeros(B, device=dev)
+        self.tau = None  # (B, 2, ndof) float32, allocated by run_with_torque
         return self
 
     def _prep_struct(self, keep: list) -> _native.MPCPrep:
@@ -245,6 +246,31 @@ class MPCControllerHIP(BaseMPCController):
                                           self.foot_wrench.data_ptr(), solver._stream_ptr())
         _native.check(rc, "srbd_u0_wrench")
         return self.foot_wrench, self.cost
+
+    def run_with_torque(self, contact_jacobian: torch.Tensor, contact_bool: torch.Tensor
+                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """run() plus the stance feed-forward joint torque the wrench feeds
+        (LegController.update_ff_torque, leg_controller.py:87-95, after
+        BipedController._run_stance_leg_controller, biped_controller.py:144-146), computed in the
+        wrench kernel's epilogue: tau (B,2,ndof) float32 = J[:,l]^T wrench[:,l] on stance legs, 0 on
+        swing legs. contact_jacobian (B,2,6,ndof) float32 (LegControllerData.J), contact_bool (B,2)."""
+        N, B = self.horizon_length, self.num_envs
+        J = _f32(contact_jacobian, self.device)
+        cb = _f32(contact_bool, self.device)
+        if J.dim() != 4 or J.shape[:3] != (B, 2, 6) or cb.shape != (B, 2):
+            raise ValueError(f"contact_jacobian must be ({B},2,6,ndof) and contact_bool ({B},2)")
+        ndof = J.shape[3]
+        if self.tau is None or self.tau.shape != (B, 2, ndof):
+            self.tau = torch.empty((B, 2, ndof), dtype=torch.float32, device=self.device)
+        self.prepare()
+        out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
+        self.solution = out
+        rot = _f32(self.state_estimate_data.rotation_body, self.device)
+        rc = _native.lib().srbd_u0_wrench_torque(N, B, out[0].data_ptr(), rot.data_ptr(), self.foot_wrench.data_ptr(),
+                                                 ndof, J.data_ptr(), cb.data_ptr(), self.tau.data_ptr(),
+                                                 solver._stream_ptr())
+        _native.check(rc, "srbd_u0_wrench_torque")
+        return self.foot_wrench, self.cost, self.tau
 
 
 # the reference's class name, for drop-in imports

@@ -8,7 +8,8 @@
 //   (mpc_controller_cusadi.py:54-95) -- fused into one thread per env that writes the 17 FP64
 //   former inputs. FP32 arithmetic follows the torch op sequence: every torch op rounds, so products
 //   and sums are evaluated with FP contraction off (no FMA).
-// u0_wrench_kernel: u0 -> body-frame foot wrench, mpc_controller_cusadi.py:186-203.
+// u0_wrench_kernel: u0 -> body-frame foot wrench, mpc_controller_cusadi.py:186-203, and optionally the
+//   stance feed-forward joint torque J^T f (leg_controller.py:87-95) from the same registers.
 // dense_scatter_kernel: CCS nonzeros -> dense (B, rows, cols), CusadiFunction.getDenseOutput
 //   (CusadiFunction.py:49-58) as a direct scatter from an inverse index map.
 #pragma once
@@ -170,7 +171,10 @@ __global__ __launch_bounds__(256) void prepare_inputs_kernel(PrepArgs a) {
 // u0 -> body-frame foot wrench (float32, (B, 2, 6)): mpc_controller_cusadi.py:186-203
 __global__ __launch_bounds__(256) void u0_wrench_kernel(int N, int batch, const double* __restrict__ x,
                                                         const float* __restrict__ rotation_body,
-                                                        float* __restrict__ wrench) {
+                                                        float* __restrict__ wrench, int ndof,
+                                                        const float* __restrict__ J,
+                                                        const float* __restrict__ contact,
+                                                        float* __restrict__ tau) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= batch) return;
   const double* u0 = x + (size_t)e * 24 * N + 12 * N;
@@ -179,12 +183,29 @@ __global__ __launch_bounds__(256) void u0_wrench_kernel(int N, int batch, const 
   u[6] = 0.0f;  // left_grm[:, 0] = 0
   u[9] = 0.0f;  // right_grm[:, 0] = 0
   const float* Rm = rotation_body + 9 * e;
-  float* w = wrench + (size_t)e * 12;
+  float w[12];
   // R^T v, then negate; blocks [lf, lm | rf, rm] with u = [lf(0..2), rf(3..5), lm(6..8), rm(9..11)]
   const int src[4] = {0, 6, 3, 9};
   for (int b = 0; b < 4; ++b) {
     const float* v = u + src[b];
     for (int i = 0; i < 3; ++i) w[3 * b + i] = -dot3f(Rm[i], Rm[3 + i], Rm[6 + i], v[0], v[1], v[2]);
+  }
+  for (int j = 0; j < 12; ++j) wrench[(size_t)e * 12 + j] = w[j];
+  if (!tau) return;
+  // stance feed-forward torque, LegController.update_ff_torque (leg_controller.py:87-95):
+  // tau_l = contact_l ? J_l^T f_l : 0 with J (B,2,6,ndof) and f_l = wrench row l; the 6-term
+  // reduction runs in index order, one rounding per op
+  for (int l = 0; l < 2; ++l) {
+    const bool on = contact[(size_t)e * 2 + l] != 0.0f;
+    const float* Jl = J + ((size_t)e * 2 + l) * 6 * ndof;
+    for (int k = 0; k < ndof; ++k) {
+      float t = 0.0f;
+      if (on) {
+        t = fm(Jl[k], w[6 * l]);
+        for (int j = 1; j < 6; ++j) t = fa(t, fm(Jl[j * ndof + k], w[6 * l + j]));
+      }
+      tau[((size_t)e * 2 + l) * ndof + k] = t;
+    }
   }
 }
 

@@ -207,6 +207,12 @@ struct RegCtx {
 
   // -------------------------------------------------------------------- factorise ----
   __device__ void factor() {
+    factor_build();
+    factor_chain();
+  }
+
+  // Phi_u foot inverses and the S_ii blocks (parallel over the wave)
+  __device__ void factor_build() {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *DV = at(Lo::DV), *PHs = at(Lo::TV);  // PHs: scratch, TV is dead here
     const double *Gf = at(Lo::Gf), *Hu = at(Lo::Hu), *Nd = at(Lo::Nd), *K0 = at(Lo::K0), *K1 = at(Lo::K1);
@@ -300,6 +306,11 @@ struct RegCtx {
     }
     __syncthreads();
     PROF_ADD(1);
+  }
+
+  __device__ void factor_chain() {
+    const int lane = fresh_lane();
+    double* DV = at(Lo::DV);
     // Twisted block recursion (see pdipm_srbd.hpp FastCtx::factor): group 0 (lanes 0..15) forward,
     // group 1 (lanes 16..31) backward in pi-permuted coordinates, middle block by group 0. Row r of
     // V = D^-1 Cg^T is computed by lane r; X = Cg V needs rows {r, 6, 7, 8} (r < 3) or {r, r + 6}
@@ -809,6 +820,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     PROF_ADD_CTX(C, 0);
 #ifdef SRBD_REPEAT_PHASE
     if (SRBD_REPEAT_PHASE == 2) C.factor();
+    if (SRBD_REPEAT_PHASE == 4) C.factor_build();
 #endif
     C.factor();
 #ifdef SRBD_REPEAT_PHASE

@@ -411,11 +411,19 @@ int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* p, double* 
 
 int srbd_u0_wrench(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
                    void* stream) {
-  if (!horizon_ok(horizon) || batch < 0 || (batch > 0 && (!x || !rotation_body || !foot_wrench)))
-    return set_error(kErrInvalid, "srbd_u0_wrench: bad arguments");
+  return srbd_u0_wrench_torque(horizon, batch, x, rotation_body, foot_wrench, 0, nullptr, nullptr, nullptr, stream);
+}
+
+int srbd_u0_wrench_torque(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
+                          int ndof, const float* contact_jacobian, const float* contact_bool, float* tau,
+                          void* stream) {
+  const bool torque = tau != nullptr;
+  if (!horizon_ok(horizon) || batch < 0 || (batch > 0 && (!x || !rotation_body || !foot_wrench)) ||
+      (torque && (ndof < 1 || ndof > 64 || (batch > 0 && (!contact_jacobian || !contact_bool)))))
+    return set_error(kErrInvalid, "srbd_u0_wrench_torque: bad arguments");
   if (batch == 0) return 0;
   hipLaunchKernelGGL(srbd::u0_wrench_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, horizon,
-                     batch, x, rotation_body, foot_wrench);
+                     batch, x, rotation_body, foot_wrench, ndof, contact_jacobian, contact_bool, tau);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "u0_wrench_kernel launch");
 }

@@ -145,6 +145,14 @@ int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* prep, doubl
 int srbd_u0_wrench(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
                    void* stream);
 
+/* srbd_u0_wrench plus the stance feed-forward joint torque of LegController.update_ff_torque
+ * (leg_controller.py:87-95; fed by BipedController._run_stance_leg_controller,
+ * biped_controller.py:144-146): tau (B,2,ndof) float32 = contact_bool[b,l] != 0 ? J[b,l]^T wrench[b,l]
+ * : 0, with contact_jacobian (B,2,6,ndof) and contact_bool (B,2) float32. tau == NULL skips it. */
+int srbd_u0_wrench_torque(int horizon, int batch, const double* x, const float* rotation_body, float* foot_wrench,
+                          int ndof, const float* contact_jacobian, const float* contact_bool, float* tau,
+                          void* stream);
+
 /* CusadiFunction.getDenseOutput (CusadiFunction.py:49-58) as one scatter: dense (B, rc) row-major
  * from nonzeros (B, nnz) through inverse_index[rc] (nonzero index of each dense entry, or -1). */
 int srbd_dense_scatter(int batch, int nnz, int rc, const int* inverse_index, const double* values,

@@ -130,3 +130,14 @@ def u0_wrench(N, x, rotation_body):
         out.append(-np.stack([_dot3(Rm[:, 0, i], Rm[:, 1, i], Rm[:, 2, i], v[:, 0], v[:, 1], v[:, 2])
                               for i in range(3)], axis=1))
     return np.concatenate(out, axis=1).reshape(-1, 2, 6)
+
+
+def stance_torque(wrench, J, contact_bool):
+    """leg_controller.py:87-95: tau[b,l] = J[b,l]^T wrench[b,l] where contact_bool[b,l] != 0, else 0.
+    float32, the 6-term sum in index order with one rounding per op (as the kernel)."""
+    w = wrench.astype(f32)
+    J = J.astype(f32)
+    t = J[:, :, 0, :] * w[:, :, 0:1]
+    for j in range(1, 6):
+        t = (t + J[:, :, j, :] * w[:, :, j:j + 1]).astype(f32)
+    return np.where(contact_bool[:, :, None] != 0, t, f32(0.0)).astype(f32)

@@ -177,6 +177,59 @@ def test_u0_wrench_matches_oracle():
     assert np.array_equal(out.cpu().numpy(), mpc_io.u0_wrench(N, x, R))
 
 
+def _torque_inputs(B, ndof, seed):
+    rng = np.random.default_rng(seed)
+    J = rng.normal(0, 0.3, (B, 2, 6, ndof)).astype(np.float32)
+    cb = (rng.uniform(size=(B, 2)) < 0.7).astype(np.float32)
+    cb[0] = 0.0  # both legs swinging
+    cb[1] = 1.0  # double support
+    return J, cb
+
+
+@pytest.mark.parametrize("ndof", [5, 6])
+def test_stance_torque_oracle_matches_torch(ndof):
+    """The restatement against the reference's own op sequence on torch CPU
+    (leg_controller.py:87-95: J^T @ f, then torch.where on the contact flag)."""
+    B = 257
+    J, cb = _torque_inputs(B, ndof, 4)
+    w = np.random.default_rng(5).normal(0, 80, (B, 2, 6)).astype(np.float32)
+    Jt, wt, cbt = torch.from_numpy(J), torch.from_numpy(w), torch.from_numpy(cb)
+    ref = torch.empty(B, 2, ndof)
+    for leg in range(2):
+        st = (Jt[:, leg].transpose(1, 2) @ wt[:, leg].unsqueeze(-1)).squeeze(-1)
+        ref[:, leg] = torch.where(cbt[:, leg].unsqueeze(-1).bool(), st, torch.zeros_like(st))
+    got = mpc_io.stance_torque(w, J, cb)
+    assert got.dtype == np.float32
+    assert np.all(got[cb == 0] == 0.0)
+    # 6-term FP32 dot: the summation order of torch's matmul is implementation-defined
+    np.testing.assert_allclose(got, ref.numpy(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndof", [5, 6])
+def test_u0_wrench_torque_matches_oracle(ndof):
+    from biped_pympc_amd import _native, solver
+    N, B = 10, 1000
+    rng = np.random.default_rng(6)
+    x = rng.normal(0, 50, (B, 24 * N))
+    R = np.linalg.qr(rng.normal(size=(B, 3, 3)))[0].astype(np.float32)
+    J, cb = _torque_inputs(B, ndof, 7)
+    w = torch.empty((B, 2, 6), dtype=torch.float32, device="cuda")
+    tau = torch.full((B, 2, ndof), float("nan"), dtype=torch.float32, device="cuda")
+    xd, Rd, Jd, cbd = (torch.from_numpy(a).cuda() for a in (x, R, J, cb))
+    _native.check(_native.lib().srbd_u0_wrench_torque(N, B, xd.data_ptr(), Rd.data_ptr(), w.data_ptr(), ndof,
+                                                      Jd.data_ptr(), cbd.data_ptr(), tau.data_ptr(),
+                                                      solver._stream_ptr()), "wrench+torque")
+    torch.cuda.synchronize()
+    wref = mpc_io.u0_wrench(N, x, R)
+    assert np.array_equal(w.cpu().numpy(), wref)
+    assert np.array_equal(tau.cpu().numpy(), mpc_io.stance_torque(wref, J, cb))
+    # bad arguments are reported, not aborted on
+    assert _native.lib().srbd_u0_wrench_torque(N, B, xd.data_ptr(), Rd.data_ptr(), w.data_ptr(), 0,
+                                               Jd.data_ptr(), cbd.data_ptr(), tau.data_ptr(),
+                                               solver._stream_ptr()) != 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("which", ["H", "A", "G"])
 def test_dense_scatter_matches_layout(which):
@@ -212,6 +265,21 @@ def test_controller_step_matches_oracle_pipeline():
     # test_gpu_parity.SOLVER_CASES); measured worst env 3.1e-5, others <= 3e-7. BASELINE bar: 1e-4.
     assert err.max() <= 1e-4, err.max()
     assert np.median(err) <= 1e-6, np.median(err)
+
+
+@pytest.mark.gpu
+def test_controller_run_with_torque():
+    N, B, ndof = 10, 64, 5
+    st, cmd, ctrl, params, gait_args, table = random_robot(B, 22, N, gait=True)
+    J, cb = _torque_inputs(B, ndof, 8)
+    c1 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    c2 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    w1, _ = c1.run()
+    w2, _, tau = c2.run_with_torque(torch.from_numpy(J), torch.from_numpy(cb))
+    torch.cuda.synchronize()
+    assert torch.equal(w1, w2)
+    assert tau.shape == (B, 2, ndof)
+    assert np.array_equal(tau.cpu().numpy(), mpc_io.stance_torque(w2.cpu().numpy(), J, cb))
 
 
 @pytest.mark.gpu
