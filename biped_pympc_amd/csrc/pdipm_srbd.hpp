@@ -71,32 +71,32 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
 #define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
 
-// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for all 12 j (j == K included; the
-// caller overwrites S[K] afterwards)
-#define SRBD_PIVOT_BLOCK(K)                                                                          \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%0", "%12", K) SRBD_FMAC_BC("%1", "%1", "%12", K)              \
-          SRBD_FMAC_BC("%2", "%2", "%12", K) SRBD_FMAC_BC("%3", "%3", "%12", K)                       \
-              SRBD_FMAC_BC("%4", "%4", "%12", K) SRBD_FMAC_BC("%5", "%5", "%12", K)                   \
-                  SRBD_FMAC_BC("%6", "%6", "%12", K) SRBD_FMAC_BC("%7", "%7", "%12", K)               \
-                      SRBD_FMAC_BC("%8", "%8", "%12", K) SRBD_FMAC_BC("%9", "%9", "%12", K)           \
-                          SRBD_FMAC_BC("%10", "%10", "%12", K) SRBD_FMAC_BC("%11", "%11", "%12", K) "s_nop 1\n" \
-      : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]), \
-        "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11])                                              \
+// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for the 11 columns j != K (the
+// caller overwrites S[K]); row_newbcast needs K at compile time, hence one asm block per K
+#define SRBD_FMAC11(K)                                                                              \
+  SRBD_FMAC_BC("%0", "%0", "%11", K) SRBD_FMAC_BC("%1", "%1", "%11", K) SRBD_FMAC_BC("%2", "%2", "%11", K) \
+  SRBD_FMAC_BC("%3", "%3", "%11", K) SRBD_FMAC_BC("%4", "%4", "%11", K) SRBD_FMAC_BC("%5", "%5", "%11", K) \
+  SRBD_FMAC_BC("%6", "%6", "%11", K) SRBD_FMAC_BC("%7", "%7", "%11", K) SRBD_FMAC_BC("%8", "%8", "%11", K) \
+  SRBD_FMAC_BC("%9", "%9", "%11", K) SRBD_FMAC_BC("%10", "%10", "%11", K)
+#define SRBD_PIVOT11(K, a, b, c, d, e, f, g, h, i, j, l)                                             \
+  asm("s_nop 1\n" SRBD_FMAC11(K) "s_nop 1\n"                                                        \
+      : "+v"(S[a]), "+v"(S[b]), "+v"(S[c]), "+v"(S[d]), "+v"(S[e]), "+v"(S[f]), "+v"(S[g]), "+v"(S[h]), \
+        "+v"(S[i]), "+v"(S[j]), "+v"(S[l])                                                          \
       : "v"(coef))
 __device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k) {
   switch (k) {
-    case 0: SRBD_PIVOT_BLOCK(0); break;
-    case 1: SRBD_PIVOT_BLOCK(1); break;
-    case 2: SRBD_PIVOT_BLOCK(2); break;
-    case 3: SRBD_PIVOT_BLOCK(3); break;
-    case 4: SRBD_PIVOT_BLOCK(4); break;
-    case 5: SRBD_PIVOT_BLOCK(5); break;
-    case 6: SRBD_PIVOT_BLOCK(6); break;
-    case 7: SRBD_PIVOT_BLOCK(7); break;
-    case 8: SRBD_PIVOT_BLOCK(8); break;
-    case 9: SRBD_PIVOT_BLOCK(9); break;
-    case 10: SRBD_PIVOT_BLOCK(10); break;
-    default: SRBD_PIVOT_BLOCK(11); break;
+    case 0: SRBD_PIVOT11(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 1: SRBD_PIVOT11(1, 0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 2: SRBD_PIVOT11(2, 0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 3: SRBD_PIVOT11(3, 0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 4: SRBD_PIVOT11(4, 0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11); break;
+    case 5: SRBD_PIVOT11(5, 0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 11); break;
+    case 6: SRBD_PIVOT11(6, 0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11); break;
+    case 7: SRBD_PIVOT11(7, 0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11); break;
+    case 8: SRBD_PIVOT11(8, 0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11); break;
+    case 9: SRBD_PIVOT11(9, 0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11); break;
+    case 10: SRBD_PIVOT11(10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11); break;
+    default: SRBD_PIVOT11(11, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10); break;
   }
 }
 
@@ -131,10 +131,10 @@ __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (
   for (int k = 0; k < 12; ++k) {
     const double id = rcp3(bc16(Sr[k], k));
     const bool piv = (r == k);
-    const double ark = Sr[k];
-    const double coef = piv ? 0.0 : -ark * id;
-    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef (pk = row k, fused broadcast)
-    Sr[k] = piv ? -1.0 : ark * id;
+    const double t = Sr[k] * id;  // before the update: Sr[k] is not an operand of the block
+    const double coef = piv ? 0.0 : -t;
+    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef, j != k (pk = row k, fused broadcast)
+    Sr[k] = piv ? -1.0 : t;
     sc = piv ? id : sc;
   }
   // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale

@@ -19,6 +19,10 @@
 #include "pdipm_srbd.hpp"
 #include "qp_former.hpp"
 
+#ifndef SRBD_CHAIN_ATTR
+#define SRBD_CHAIN_ATTR  // diagnostic builds: __attribute__((noinline)) to read the chain's ISA alone
+#endif
+
 namespace srbd {
 
 template <int N>
@@ -308,7 +312,7 @@ struct RegCtx {
     PROF_ADD(1);
   }
 
-  __device__ void factor_chain() {
+  SRBD_CHAIN_ATTR __device__ void factor_chain() {
     const int lane = fresh_lane();
     double* DV = at(Lo::DV);
     // Twisted block recursion (see pdipm_srbd.hpp FastCtx::factor): group 0 (lanes 0..15) forward,
