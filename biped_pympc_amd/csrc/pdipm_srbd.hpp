@@ -71,19 +71,19 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
 #define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
 
-// one Gauss-Jordan pivot update: S[j] += S[j](lane K) * coef for the 11 columns j != K (the
-// caller overwrites S[K]); row_newbcast needs K at compile time, hence one asm block per K
+// one Gauss-Jordan pivot update: S[j] -= S[j](lane K) * t for the 11 columns j != K (the caller
+// overwrites S[K]); row_newbcast needs K at compile time, hence one asm block per K
 #define SRBD_FMAC11(K)                                                                              \
-  SRBD_FMAC_BC("%0", "%0", "%11", K) SRBD_FMAC_BC("%1", "%1", "%11", K) SRBD_FMAC_BC("%2", "%2", "%11", K) \
-  SRBD_FMAC_BC("%3", "%3", "%11", K) SRBD_FMAC_BC("%4", "%4", "%11", K) SRBD_FMAC_BC("%5", "%5", "%11", K) \
-  SRBD_FMAC_BC("%6", "%6", "%11", K) SRBD_FMAC_BC("%7", "%7", "%11", K) SRBD_FMAC_BC("%8", "%8", "%11", K) \
-  SRBD_FMAC_BC("%9", "%9", "%11", K) SRBD_FMAC_BC("%10", "%10", "%11", K)
+  SRBD_FMAC_BC("%0", "%0", "-%11", K) SRBD_FMAC_BC("%1", "%1", "-%11", K) SRBD_FMAC_BC("%2", "%2", "-%11", K) \
+  SRBD_FMAC_BC("%3", "%3", "-%11", K) SRBD_FMAC_BC("%4", "%4", "-%11", K) SRBD_FMAC_BC("%5", "%5", "-%11", K) \
+  SRBD_FMAC_BC("%6", "%6", "-%11", K) SRBD_FMAC_BC("%7", "%7", "-%11", K) SRBD_FMAC_BC("%8", "%8", "-%11", K) \
+  SRBD_FMAC_BC("%9", "%9", "-%11", K) SRBD_FMAC_BC("%10", "%10", "-%11", K)
 #define SRBD_PIVOT11(K, a, b, c, d, e, f, g, h, i, j, l)                                             \
   asm("s_nop 1\n" SRBD_FMAC11(K) "s_nop 1\n"                                                        \
       : "+v"(S[a]), "+v"(S[b]), "+v"(S[c]), "+v"(S[d]), "+v"(S[e]), "+v"(S[f]), "+v"(S[g]), "+v"(S[h]), \
         "+v"(S[i]), "+v"(S[j]), "+v"(S[l])                                                          \
-      : "v"(coef))
-__device__ __forceinline__ void pivot_update(double (&S)[12], double coef, int k) {
+      : "v"(t))
+__device__ __forceinline__ void pivot_update(double (&S)[12], double t, int k) {
   switch (k) {
     case 0: SRBD_PIVOT11(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
     case 1: SRBD_PIVOT11(1, 0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
@@ -115,28 +115,46 @@ __device__ __forceinline__ double dot_bc12(const double (&c)[12], double v) {
   return (a0 + a1) + a2;
 }
 
-// Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r in lane r of a 16-lane
-// DPP row; lanes 12..15 shadow row 11), by Gauss-Jordan pivoting on the diagonal. The
-// pivot row is not rescaled in place (a plain sweep would multiply every element of every row by
-// a select to special-case it): every lane keeps its row unscaled together with a scale
-// factor (1/pivot once the row has been the pivot) that is applied once at the end, so each pivot
-// costs one fused broadcast-FMA per element and lane (pivot_update; no per-element select).
+// Row r of the INVERSE of a 12x12 SPD block held one row per lane (row r = lane & 15 of a 16-lane
+// DPP row, lanes 12..15 shadowing row 11; the chains run on lanes 0..31), by Gauss-Jordan pivoting
+// on the diagonal. The pivot row is not rescaled in place (a plain sweep would multiply every
+// element of every row by a select to special-case it): every lane keeps its row unscaled together
+// with a scale factor (1/pivot once the row has been the pivot) that is applied once at the end, so
+// each pivot costs one fused broadcast-FMA per element and lane (pivot_update).
 //   pivot k (pk = row k, broadcast by row_newbcast inside the FMAs, id = 1/pk[k] by rcp3):
 //     lane r != k: a_rj <- a_rj - a_rk id pk_j  (j != k),  a_rk <- a_rk id
 //     lane k     : row unchanged except a_kk <- -1, scale <- id
+// The pivot lanes of step k are a compile-time lane set, so their special cases are exec-masked
+// 64-bit moves (2 SALU + 1 VALU each) instead of 64-bit selects (2 v_cndmask_b32 each): a_kk is
+// zeroed on them right after the broadcast (t = a_kk id = 0 makes their update a no-op), then set
+// to -1 with scale <- id after the update.
 // On exit Dr[j] = (A^-1)_rj.
-__device__ __forceinline__ void inverse_rows12(double (&Sr)[12], int r, double (&Dr)[12]) {
+template <int K>
+struct PivotLanes {  // s_and_saveexec_b64 literal (32-bit, sign-extended; lanes >= 32 are inactive)
+  static constexpr uint32_t m16 = (1u << K) | (K == 11 ? 0xF000u : 0u);
+  static constexpr int64_t value = (int32_t)(m16 | (m16 << 16));
+};
+
+template <int K>
+__device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc) {
+  const double pk = bc16(Sr[K], K);
+  uint64_t sv;
+  asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], 0\n\ts_mov_b64 exec, %[sv]"
+      : [x] "+v"(Sr[K]), [sv] "=&s"(sv)
+      : [m] "n"(PivotLanes<K>::value));
+  const double id = rcp3(pk);
+  const double t = Sr[K] * id;  // 0 on the pivot lanes
+  pivot_update(Sr, t, K);       // Sr[j] -= pk[j] t, j != K
+  Sr[K] = t;
+  asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], -1.0\n\tv_mov_b64 %[s], %[id]\n\ts_mov_b64 exec, %[sv]"
+      : [x] "+v"(Sr[K]), [s] "+v"(sc), [sv] "=&s"(sv)
+      : [id] "v"(id), [m] "n"(PivotLanes<K>::value));
+  if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
+}
+
+__device__ __forceinline__ void inverse_rows12(double (&Sr)[12], double (&Dr)[12]) {
   double sc = 1.0;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) {
-    const double id = rcp3(bc16(Sr[k], k));
-    const bool piv = (r == k);
-    const double t = Sr[k] * id;  // before the update: Sr[k] is not an operand of the block
-    const double coef = piv ? 0.0 : -t;
-    pivot_update(Sr, coef, k);  // Sr[j] += pk[j] * coef, j != k (pk = row k, fused broadcast)
-    Sr[k] = piv ? -1.0 : t;
-    sc = piv ? id : sc;
-  }
+  gj_pivot<0>(Sr, sc);
   // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
   const double nsc = -sc;
 #pragma unroll
@@ -375,7 +393,7 @@ struct FastCtx {
             }
           }
           if (act && !(mstep && g == 1)) {
-            inverse_rows12(Sr, r, Dr);
+            inverse_rows12(Sr, Dr);
             if (own) {
               double* Di = DV + 78 * i;
 #pragma unroll

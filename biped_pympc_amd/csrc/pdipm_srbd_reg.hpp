@@ -380,15 +380,14 @@ struct RegCtx {
           }
         }
         if (act && !(mstep && g == 1)) {
-          inverse_rows12(Sr, r, Dr);
-          if (own) {
-            double* Di = DV + 78 * i;
+          inverse_rows12(Sr, Dr);
+          // every lane writes its whole row: (r, c) and (c, r) share a packed slot, so each slot is
+          // written twice with the two (rounding-different) halves of the symmetric inverse; the
+          // later ds_write in program order wins, deterministically (shadow lanes 12..15 repeat row
+          // 11 bit for bit). Cheaper than 12 per-element exec-masked stores.
+          double* Di = DV + 78 * i;
 #pragma unroll
-            for (int c = 0; c < 12; ++c) {
-              const int pc = g ? perm12c(c) : c;
-              if (pc <= pr) Di[offs[c]] = Dr[c];
-            }
-          }
+          for (int c = 0; c < 12; ++c) Di[offs[c]] = Dr[c];
         }
       }
     }
