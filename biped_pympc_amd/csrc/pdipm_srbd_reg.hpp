@@ -61,6 +61,34 @@ __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x
       : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8));
 }
 
+// lane i of every 16-lane row <- lane i - 6 (rows 9..11 fetch rows 3..5)
+__device__ __forceinline__ double shr6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x116, 0xF, 0xF, true); }
+
+// (C w)_r and (C^T y)_r of the compact stage coupling for one vector held one element per lane:
+// C has the diagonal, rows 0..2 x columns 6..8 and (r, r + 6) for 3 <= r < 6, so each is a local
+// product, one row shift and three broadcast-FMAs (instead of a dense 12-term broadcast dot).
+//   C w  : d w_r + b w_{r+6} + a0 w_6 + a1 w_7 + a2 w_8     (a* nonzero for r < 3, b for 3 <= r < 6)
+//   C^T y: d y_r + b y_{r-6} + a0 y_0 + a1 y_1 + a2 y_2     (a* nonzero for 6 <= r < 9, b for r >= 9)
+struct CoupleRow {
+  double d, b, a0, a1, a2;
+};
+__device__ __forceinline__ double couple_cw(const CoupleRow& c, double w) {
+  double acc = c.d * w + c.b * shl6(w);
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%1", "%2", 6) SRBD_FMAC_BC("%0", "%1", "%3", 7)
+      SRBD_FMAC_BC("%0", "%1", "%4", 8) "s_nop 1\n"
+      : "+v"(acc)
+      : "v"(w), "v"(c.a0), "v"(c.a1), "v"(c.a2));
+  return acc;
+}
+__device__ __forceinline__ double couple_cty(const CoupleRow& c, double y) {
+  double acc = c.d * y + c.b * shr6(y);
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%1", "%2", 0) SRBD_FMAC_BC("%0", "%1", "%3", 1)
+      SRBD_FMAC_BC("%0", "%1", "%4", 2) "s_nop 1\n"
+      : "+v"(acc)
+      : "v"(y), "v"(c.a0), "v"(c.a1), "v"(c.a2));
+  return acc;
+}
+
 // element (c, b) of a compact M / C block (c or b runtime)
 __device__ __forceinline__ double cel(const double* cc, int c, int b) {
   if (b == c) return cc[c];
@@ -474,14 +502,22 @@ struct RegCtx {
       const int pr = g ? perm12(r) : r;
       const int cnt = g ? nb : nf;
       const double* cc = at(Lo::Cc) + 24 * g;
-      double Crow[12], Ccol[12];
+      CoupleRow Cr, Ct;  // row r of Cg and of Cg^T (compact layout, see the header)
       int offs[12];
 #pragma unroll
       for (int j = 0; j < 12; ++j) {
-        Crow[j] = cel(cc, r, j);
-        Ccol[j] = cel(cc, j, r);
         offs[j] = sym_idx(pr, g ? perm12c(j) : j);
       }
+      Cr.d = cc[r];
+      Cr.b = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
+      Cr.a0 = r < 3 ? cc[12 + 3 * r] : 0.0;
+      Cr.a1 = r < 3 ? cc[13 + 3 * r] : 0.0;
+      Cr.a2 = r < 3 ? cc[14 + 3 * r] : 0.0;
+      Ct.d = cc[r];
+      Ct.b = r >= 9 ? cc[12 + r] : 0.0;
+      Ct.a0 = (r >= 6 && r < 9) ? cc[12 + r - 6] : 0.0;
+      Ct.a1 = (r >= 6 && r < 9) ? cc[15 + r - 6] : 0.0;
+      Ct.a2 = (r >= 6 && r < 9) ? cc[18 + r - 6] : 0.0;
       double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
 #pragma unroll
       for (int k = 0; k <= T; ++k) wv[k] = 0.0;
@@ -492,7 +528,7 @@ struct RegCtx {
         const bool act = mstep ? true : (t < cnt);
         const bool prev = mstep ? (cnt >= 1) : (t >= 1);
         double cw = 0.0;
-        if (act && prev) cw = dot_bc12(Crow, w);
+        if (act && prev) cw = couple_cw(Cr, w);
         double mv = 0.0;
         if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
         if (act && !(mstep && g == 1)) {
@@ -522,7 +558,7 @@ struct RegCtx {
           double Dr[12];
 #pragma unroll
           for (int k = 0; k < 12; ++k) Dr[k] = Di[offs[k]];
-          const double sc = dot_bc12(Ccol, y);  // Cg^T y_prev
+          const double sc = couple_cty(Ct, y);  // Cg^T y_prev
           y = wprev - dot_bc12(Dr, sc);
           if (own) QV[12 * i + pr] = y;
         }
