@@ -19,8 +19,8 @@
 #include "pdipm_srbd.hpp"
 #include "qp_former.hpp"
 
-#ifndef SRBD_CHAIN_ATTR
-#define SRBD_CHAIN_ATTR  // diagnostic builds: __attribute__((noinline)) to read the chain's ISA alone
+#ifndef SRBD_PHASE_ATTR
+#define SRBD_PHASE_ATTR  // diagnostic builds: __attribute__((noinline)) to read one phase ISA alone
 #endif
 
 namespace srbd {
@@ -47,18 +47,24 @@ __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6;
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
 // acc[i] += v[i](lane 6) c6 + v[i](lane 7) c7 + v[i](lane 8) c8 for 4 elements (the rows 6..8 term
-// of the Schur update X = C V)
+// of the Schur update X = C V); kNeg: acc[i] -= the same
+#define SRBD_ROWS678_4(N6, N7, N8)                                                                  \
+  asm("s_nop 1\n"                                                                                   \
+      SRBD_FMAC_BC("%0", "%4", N6, 6) SRBD_FMAC_BC("%1", "%5", N6, 6) SRBD_FMAC_BC("%2", "%6", N6, 6) \
+      SRBD_FMAC_BC("%3", "%7", N6, 6) SRBD_FMAC_BC("%0", "%4", N7, 7) SRBD_FMAC_BC("%1", "%5", N7, 7) \
+      SRBD_FMAC_BC("%2", "%6", N7, 7) SRBD_FMAC_BC("%3", "%7", N7, 7) SRBD_FMAC_BC("%0", "%4", N8, 8) \
+      SRBD_FMAC_BC("%1", "%5", N8, 8) SRBD_FMAC_BC("%2", "%6", N8, 8) SRBD_FMAC_BC("%3", "%7", N8, 8) \
+      "s_nop 1\n"                                                                                   \
+      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)                                                      \
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8))
+template <bool kNeg = false>
 __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x2, double& x3, double v0,
                                                double v1, double v2, double v3, double c6, double c7,
                                                double c8) {
-  asm("s_nop 1\n"
-      SRBD_FMAC_BC("%0", "%4", "%8", 6) SRBD_FMAC_BC("%1", "%5", "%8", 6) SRBD_FMAC_BC("%2", "%6", "%8", 6)
-      SRBD_FMAC_BC("%3", "%7", "%8", 6) SRBD_FMAC_BC("%0", "%4", "%9", 7) SRBD_FMAC_BC("%1", "%5", "%9", 7)
-      SRBD_FMAC_BC("%2", "%6", "%9", 7) SRBD_FMAC_BC("%3", "%7", "%9", 7) SRBD_FMAC_BC("%0", "%4", "%10", 8)
-      SRBD_FMAC_BC("%1", "%5", "%10", 8) SRBD_FMAC_BC("%2", "%6", "%10", 8) SRBD_FMAC_BC("%3", "%7", "%10", 8)
-      "s_nop 1\n"
-      : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
-      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8));
+  if constexpr (kNeg)
+    SRBD_ROWS678_4("-%8", "-%9", "-%10");
+  else
+    SRBD_ROWS678_4("%8", "%9", "%10");
 }
 
 // lane i of every 16-lane row <- lane i - 6 (rows 9..11 fetch rows 3..5)
@@ -109,7 +115,7 @@ __device__ __forceinline__ double mcol(const double* mc, int j, const double* v)
   else if (j >= 9) a += mc[21 + j - 9] * v[j - 6];
   return a;
 }
-// dense 12-term row / column products (N block)
+// dense 12-term row product (N block; rows are lane-dependent, so no per-row sparsity)
 __device__ __forceinline__ double drow12(const double* row, const double* v) {
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
@@ -120,16 +126,21 @@ __device__ __forceinline__ double drow12(const double* row, const double* v) {
   }
   return (a0 + a1) + a2;
 }
-__device__ __forceinline__ double dcol12(const double* mat, int col, const double* v) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    a0 += mat[r * 12 + col] * v[r];
-    a1 += mat[(r + 4) * 12 + col] * v[r + 4];
-    a2 += mat[(r + 8) * 12 + col] * v[r + 8];
+// (N^T v)_col over the stage u-block's sparsity: rows {0,1,2,6,7,8} are dense, rows {3+p, 9+p}
+// (p = col % 3) hold only the force columns col < 6 (srbd_constraints.py:83-142 through B_d; the
+// stored zeros make the formula exact for every col); kForce = false skips them (col >= 6 known)
+template <bool kForce = true>
+__device__ __forceinline__ double ncol(const double* nd, int col, const double* v, int p) {
+  double a0 = nd[col] * v[0] + nd[12 + col] * v[1];
+  double a1 = nd[24 + col] * v[2] + nd[72 + col] * v[6];
+  double a2 = nd[84 + col] * v[7] + nd[96 + col] * v[8];
+  if (kForce) {
+    a0 += nd[12 * (3 + p) + col] * v[3 + p];
+    a1 += nd[12 * (9 + p) + col] * v[9 + p];
   }
   return (a0 + a1) + a2;
 }
+
 // (G xu)_k over the 4 columns of row k's foot
 __device__ __forceinline__ double grow4(const double* gf, int k, const double* xu) {
   const int f = k >> 3;
@@ -162,7 +173,7 @@ struct RegCtx {
   }
 
   // --------------------------------------------------------------------- residuals ----
-  __device__ double residuals() {
+  SRBD_PHASE_ATTR __device__ double residuals() {
     const int lane = fresh_lane();
     const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
                  *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
@@ -198,7 +209,7 @@ struct RegCtx {
           }
           gz = g0 + g1;
         }
-        double ay = dcol12(Nd, j, Y + 12 * i);
+        double ay = ncol(Nd, j, Y + 12 * i, j % 3);
         if (j == 6) ay += SG[6] * Y[nx + 2 * i];
         if (j == 9) ay += SG[7] * Y[nx + 2 * i + 1];
         RXu[c] = (v + gz) + ay;
@@ -244,7 +255,7 @@ struct RegCtx {
   }
 
   // Phi_u foot inverses and the S_ii blocks (parallel over the wave)
-  __device__ void factor_build() {
+  SRBD_PHASE_ATTR __device__ void factor_build() {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *DV = at(Lo::DV), *PHs = at(Lo::TV);  // PHs: scratch, TV is dead here
     const double *Gf = at(Lo::Gf), *Hu = at(Lo::Hu), *Nd = at(Lo::Nd), *K0 = at(Lo::K0), *K1 = at(Lo::K1);
@@ -340,7 +351,7 @@ struct RegCtx {
     PROF_ADD(1);
   }
 
-  SRBD_CHAIN_ATTR __device__ void factor_chain() {
+  SRBD_PHASE_ATTR __device__ void factor_chain() {
     const int lane = fresh_lane();
     double* DV = at(Lo::DV);
     // Twisted block recursion (see pdipm_srbd.hpp FastCtx::factor): group 0 (lanes 0..15) forward,
@@ -388,15 +399,24 @@ struct RegCtx {
               else if (c < 6) v += Dr[c + 6] * cc[21 + c - 3];
               V[c] = v;
             }
+            if (!mstep) {  // S - X accumulated in place
 #pragma unroll
-            for (int c = 0; c < 12; ++c) X[c] = crd * V[c] + crb * shl6(V[c]);
+              for (int c = 0; c < 12; ++c) Sr[c] = (Sr[c] - crd * V[c]) - crb * shl6(V[c]);
 #pragma unroll
-            for (int c = 0; c < 12; c += 4)  // + rows 6..8 of V through fused broadcast-FMAs
-              fmac_rows678_4(X[c], X[c + 1], X[c + 2], X[c + 3], V[c], V[c + 1], V[c + 2], V[c + 3], cra0, cra1,
-                             cra2);
-            if (!(mstep && g == 1)) {
+              for (int c = 0; c < 12; c += 4)  // - rows 6..8 of V through fused broadcast-FMAs
+                fmac_rows678_4<true>(Sr[c], Sr[c + 1], Sr[c + 2], Sr[c + 3], V[c], V[c + 1], V[c + 2], V[c + 3],
+                                     cra0, cra1, cra2);
+            } else {  // middle step: group 1's X is handed to group 0 below
 #pragma unroll
-              for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
+              for (int c = 0; c < 12; ++c) X[c] = crd * V[c] + crb * shl6(V[c]);
+#pragma unroll
+              for (int c = 0; c < 12; c += 4)  // + rows 6..8 of V through fused broadcast-FMAs
+                fmac_rows678_4(X[c], X[c + 1], X[c + 2], X[c + 3], V[c], V[c + 1], V[c + 2], V[c + 3], cra0,
+                               cra1, cra2);
+              if (g == 0) {
+#pragma unroll
+                for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
+              }
             }
           }
         }
@@ -425,7 +445,7 @@ struct RegCtx {
 
   // ------------------------------------------------------------------------ solve ----
   // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
-  __device__ void solve(int mode, double smu) {
+  SRBD_PHASE_ATTR __device__ void solve(int mode, double smu) {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
@@ -585,7 +605,8 @@ struct RegCtx {
         const int f = lane & 1;
         double av[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) av[a] = dcol12(Nd, foot_colj(f, a), yi);
+        for (int a = 0; a < 3; ++a) av[a] = ncol(Nd, foot_colj(f, a), yi, a);
+        av[3] = ncol<false>(Nd, foot_colj(f, 3), yi, 0);
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
@@ -595,8 +616,8 @@ struct RegCtx {
         }
       } else {
         const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
-        const double a6 = dcol12(Nd, 6, yi), a9 = dcol12(Nd, 9, yi);
-        const double a8 = dcol12(Nd, 8, yi), a11 = dcol12(Nd, 11, yi);
+        const double a6 = ncol<false>(Nd, 6, yi, 0), a9 = ncol<false>(Nd, 9, yi, 0);
+        const double a8 = ncol<false>(Nd, 8, yi, 0), a11 = ncol<false>(Nd, 11, yi, 0);
         TV[b + 6] -= SG[0] * a6;
         TV[b + 9] -= SG[2] * a9;
         TV[b + 8] -= SG[1] * a8;
