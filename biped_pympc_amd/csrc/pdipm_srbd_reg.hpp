@@ -297,55 +297,73 @@ struct RegCtx {
       }
     }
     __syncthreads();
-    // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in three divergence-free passes over the class-sorted
-    // entry table (TRI = c_tab.dvo): rows {3,4,5,9,10,11} of N hold one entry per foot (position
-    // r % 3), so an entry touching them needs 10 (one sparse index) or 4 (two) FMAs instead of 40
-    auto kval = [&](int i, int r, int c) { return (i == 0 ? K0 : K1)[r * (r + 1) / 2 + c]; };
-    for (int e = lane; e < 21 * N; e += 64) {  // dense x dense
-      const int i = e / 21, rc = TRI[e % 21], r = rc & 15, c = rc >> 4;
-      double v = kval(i, r, c);
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const double* ph_ = PHs + 20 * i + 10 * f;
-        double vc[4], vr[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          vr[a] = Nd[r * 12 + foot_colj(f, a)];
-          vc[a] = Nd[c * 12 + foot_colj(f, a)];
-        }
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) t += ph_[sym_idx(a, b)] * vc[b];
-          v += vr[a] * t;
-        }
-      }
-      DV[78 * i + r * (r + 1) / 2 + c] = v;
-    }
-    for (int e = lane; e < 36 * N; e += 64) {  // sparse x dense
-      const int i = e / 36, rc = TRI[21 + e % 36], r = rc & 15, c = rc >> 4;
-      const bool rs = (r % 6) >= 3;
-      const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
-      double v = kval(i, r, c);
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const double* ph_ = PHs + 20 * i + 10 * f;
-        double t = 0.0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) t += ph_[sym_idx(as, b)] * Nd[dn * 12 + foot_colj(f, b)];
-        v += Nd[sp * 12 + foot_colj(f, as)] * t;
-      }
-      DV[78 * i + r * (r + 1) / 2 + c] = v;
-    }
-    for (int e = lane; e < 21 * N; e += 64) {  // sparse x sparse
-      const int i = e / 21, rc = TRI[57 + e % 21], r = rc & 15, c = rc >> 4;
-      const int ar = r % 3, ac = c % 3;
-      double v = kval(i, r, c);
+    // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in two divergence-free passes over the class-sorted entry
+    // table (TRI = c_tab.dvo: 21 dense x dense entries, then 57 with a sparse index): an entry
+    // touching rows {3,4,5,9,10,11} of N needs 10 FMAs instead of 40
+    // Each lane keeps ONE entry (r, c) for the whole pass, so its table entry, N rows and K values
+    // are loaded once; only Phi_f^-1 (PHs) changes with the stage.
+    if (lane < 63) {  // dense x dense: lane = 21 q + k -> entry k of stages 3 t + q
+      const int q = lane / 21, k = lane - 21 * q;
+      const int rc = TRI[k], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
+      double vr[2][4], vc[2][4];
 #pragma unroll
       for (int f = 0; f < 2; ++f)
-        v += Nd[r * 12 + foot_colj(f, ar)] * PHs[20 * i + 10 * f + sym_idx(ar, ac)] * Nd[c * 12 + foot_colj(f, ac)];
-      DV[78 * i + r * (r + 1) / 2 + c] = v;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          vr[f][a] = Nd[r * 12 + foot_colj(f, a)];
+          vc[f][a] = Nd[c * 12 + foot_colj(f, a)];
+        }
+      const double k0 = K0[sy], k1 = K1[sy];
+#pragma unroll
+      for (int t = 0; t < (N + 2) / 3; ++t) {
+        const int i = 3 * t + q;
+        if (i < N) {
+          double v = i == 0 ? k0 : k1;
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const double* ph_ = PHs + 20 * i + 10 * f;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+              double tt = 0.0;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) tt += ph_[sym_idx(a, b)] * vc[f][b];
+              v += vr[f][a] * tt;
+            }
+          }
+          DV[78 * i + sy] = v;
+        }
+      }
+    }
+    if (lane < 57) {  // the 57 entries with a sparse index (rows {3,4,5,9,10,11} of N hold one entry
+                      // per foot, at position r % 3), one stage per trip; for a sparse x sparse entry
+                      // the 4-term sum over the "dense" index meets N's zeros, so it is exact too
+      const int rc = TRI[21 + lane], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
+      const bool rs = (r % 6) >= 3;
+      const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
+      double nd[2][4], ns[2];
+      int po[4];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nd[f][b] = Nd[dn * 12 + foot_colj(f, b)];
+        ns[f] = Nd[sp * 12 + foot_colj(f, as)];
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
+      const double k0 = K0[sy], k1 = K1[sy];
+#pragma unroll 2
+      for (int i = 0; i < N; ++i) {
+        double v = i == 0 ? k0 : k1;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const double* ph_ = PHs + 20 * i + 10 * f;
+          double tt = 0.0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) tt += ph_[po[b]] * nd[f][b];
+          v += ns[f] * tt;
+        }
+        DV[78 * i + sy] = v;
+      }
     }
     __syncthreads();
     PROF_ADD(1);
