@@ -178,12 +178,25 @@ struct RegCtx {
     const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
                  *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
     double *RXu = at(Lo::RXu), *REm = at(Lo::REm);
+    // this lane's rows of f, h, b (global, L2-resident): all loads issued up front with clamped
+    // indices, so the phase waits for one L2 round trip instead of one per guarded chunk
+    double fx[SX], fu[SX], bv[SE], hv[SI];
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {
+      const int c = min(lane + 64 * t, nx - 1);
+      fx[t] = fg[c];
+      fu[t] = fg[nx + c];
+    }
+#pragma unroll
+    for (int t = 0; t < SE; ++t) bv[t] = bg[min(lane + 64 * t, p - 1)];
+#pragma unroll
+    for (int t = 0; t < SI; ++t) hv[t] = hg[min(lane + 64 * t, m - 1)];
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
       const int c = lane + 64 * t;
       if (c < nx) {
         const int k = c / 12 + 1, j = c % 12;
-        const double v = Hu[12 + j] * X[c] + fg[c];
+        const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         if (k < N) ay += mcol(Mc, j, Y + 12 * k);
         rxx[t] = v + ay;
@@ -194,7 +207,7 @@ struct RegCtx {
       const int c = lane + 64 * t;
       if (c < nx) {
         const int i = c / 12, j = c % 12;
-        const double v = Hu[j] * X[nx + c] + fg[nx + c];
+        const double v = Hu[j] * X[nx + c] + fu[t];
         double gz = 0.0;
         const int f = foot_of(j);
         if (f >= 0) {
@@ -229,7 +242,7 @@ struct RegCtx {
           const int i = (e - nx) / 2, w = (e - nx) % 2;
           v = SG[6 + w] * X[nx + 12 * i + (w ? 9 : 6)];
         }
-        re[t] = v - bg[e];
+        re[t] = v - bv[t];
         if (e >= nx) REm[e - nx] = re[t];
       }
     }
@@ -240,7 +253,7 @@ struct RegCtx {
       if (q < m) {
         const int i = q / 16, k = q % 16;
         const double v = grow4(Gf, k, X + nx + 12 * i);
-        rs[t] = (v + s[t]) - hg[q];
+        rs[t] = (v + s[t]) - hv[t];
         sz += s[t] * z[t];
       }
     }
