@@ -69,7 +69,11 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
 // entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
 // block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
+#ifdef SRBD_EXP_NODPP  // timing experiment only (wrong results): plain FMAs, no broadcast
+#define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64 " D ", " S ", " C "\n"
+#else
 #define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
+#endif
 
 // one Gauss-Jordan pivot update: S[j] -= S[j](lane K) * t for the 11 columns j != K (the caller
 // overwrites S[K]); row_newbcast needs K at compile time, hence one asm block per K
@@ -135,9 +139,20 @@ struct PivotLanes {  // s_and_saveexec_b64 literal (32-bit, sign-extended; lanes
   static constexpr int64_t value = (int32_t)(m16 | (m16 << 16));
 };
 
+#ifdef SRBD_EXP_GJ_NODEP  // timing experiment only (wrong results): pivots read the input block,
+                          // which removes the pivot-to-pivot dependency and keeps the work
+#endif
 template <int K>
-__device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc) {
+__device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc
+#ifdef SRBD_EXP_GJ_NODEP
+                                         , const double (&g_exp_s0_reg)[12]
+#endif
+) {
+#ifdef SRBD_EXP_GJ_NODEP
+  const double pk = bc16(g_exp_s0_reg[K], K);
+#else
   const double pk = bc16(Sr[K], K);
+#endif
   uint64_t sv;
   asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], 0\n\ts_mov_b64 exec, %[sv]"
       : [x] "+v"(Sr[K]), [sv] "=&s"(sv)
@@ -149,12 +164,23 @@ __device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc) {
   asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], -1.0\n\tv_mov_b64 %[s], %[id]\n\ts_mov_b64 exec, %[sv]"
       : [x] "+v"(Sr[K]), [s] "+v"(sc), [sv] "=&s"(sv)
       : [id] "v"(id), [m] "n"(PivotLanes<K>::value));
+#ifdef SRBD_EXP_GJ_NODEP
+  if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc, g_exp_s0_reg);
+#else
   if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
+#endif
 }
 
 __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], double (&Dr)[12]) {
   double sc = 1.0;
+#ifdef SRBD_EXP_GJ_NODEP
+  double s0[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) s0[j] = Sr[j];
+  gj_pivot<0>(Sr, sc, s0);
+#else
   gj_pivot<0>(Sr, sc);
+#endif
   // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
   const double nsc = -sc;
 #pragma unroll

@@ -43,6 +43,54 @@ __device__ __forceinline__ int foot_pos(int j) { return j < 6 ? j % 3 : 3; }
 __host__ __device__ constexpr int foot_colj(int f, int a) { return a < 3 ? a + 3 * f : 7 + 3 * f; }
 __host__ __device__ constexpr int perm12c(int j) { return j < 6 ? j + 6 : j - 6; }
 
+// Block position of stage i inside DV: the forward group's step t (stage t) at 2t, the backward
+// group's step t (stage N-1-t) at 2t+1, the middle stage at N-1. A step's two blocks then sit at
+// 1248 t + 624 g bytes, so with the group term folded into the lane's offsets every block access of
+// the chains is a fixed VGPR + an immediate offset (no per-step address arithmetic).
+template <int N>
+__host__ __device__ constexpr int dv_pos(int i) {
+  return i < N / 2 ? 2 * i : (i == N / 2 ? N - 1 : 2 * (N - 1 - i) + 1);
+}
+constexpr int kDvBytes = 78 * 8;  // one packed-lower 12x12 block
+
+// Byte offset, inside a step's block pair, of element (row r, column c) of chain lane l (group
+// g = l >> 4, row r = min(l & 15, 11), both in the group's coordinates): packed-lower slot of
+// (pi^g r, pi^g c) + 624 g. One row of 12 per lane, read once per phase instead of recomputed.
+struct ChainOffs {
+  uint32_t o[32][12];
+};
+constexpr int sym_idx_c(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
+constexpr ChainOffs make_chain_offs() {
+  ChainOffs t{};
+  for (int l = 0; l < 32; ++l) {
+    const int g = l >> 4, r = (l & 15) < 12 ? (l & 15) : 11;
+    const int pr = g ? perm12c(r) : r;
+    for (int c = 0; c < 12; ++c) t.o[l][c] = (uint32_t)(8 * sym_idx_c(pr, g ? perm12c(c) : c) + kDvBytes * g);
+  }
+  return t;
+}
+static __constant__ ChainOffs c_choffs = make_chain_offs();
+
+// this chain lane's 12 offsets (three 16-byte loads from the constant table)
+__device__ __forceinline__ void load_chain_offs(int lane, uint32_t (&offs)[12]) {
+  const uint4* p = reinterpret_cast<const uint4*>(c_choffs.o[lane & 31]);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint4 v = p[q];
+    offs[4 * q] = v.x;
+    offs[4 * q + 1] = v.y;
+    offs[4 * q + 2] = v.z;
+    offs[4 * q + 3] = v.w;
+  }
+}
+// double at DV byte offset off + imm (imm compile-time: folded into the ds instruction)
+__device__ __forceinline__ double& dv_at(double* DV, uint32_t off, int imm) {
+  return *reinterpret_cast<double*>(reinterpret_cast<char*>(DV) + off + imm);
+}
+__device__ __forceinline__ double dv_at(const double* DV, uint32_t off, int imm) {
+  return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(DV) + off + imm);
+}
+
 // lane i of every 16-lane row <- lane i + 6 (rows 3..5 fetch rows 9..11)
 __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x106, 0xF, 0xF, true); }
 
@@ -343,7 +391,7 @@ struct RegCtx {
               v += vr[f][a] * tt;
             }
           }
-          DV[78 * i + sy] = v;
+          DV[78 * dv_pos<N>(i) + sy] = v;
         }
       }
     }
@@ -375,7 +423,7 @@ struct RegCtx {
           for (int b = 0; b < 4; ++b) tt += ph_[po[b]] * nd[f][b];
           v += ns[f] * tt;
         }
-        DV[78 * i + sy] = v;
+        DV[78 * dv_pos<N>(i) + sy] = v;
       }
     }
     __syncthreads();
@@ -401,9 +449,8 @@ struct RegCtx {
       const double cra0 = r < 3 ? cc[12 + 3 * r] : 0.0, cra1 = r < 3 ? cc[13 + 3 * r] : 0.0,
                    cra2 = r < 3 ? cc[14 + 3 * r] : 0.0;
       const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
-      int offs[12];  // packed-lower offset of (pr, column c in group coordinates)
-#pragma unroll
-      for (int c = 0; c < 12; ++c) offs[c] = sym_idx(pr, g ? perm12c(c) : c);
+      uint32_t offs[12];  // byte offset of (pr, column c in group coordinates) in a step's blocks
+      load_chain_offs(lane, offs);
       double Dr[12];
 #pragma unroll
       for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
@@ -417,10 +464,12 @@ struct RegCtx {
         double Sr[12], X[12];
 #pragma unroll
         for (int c = 0; c < 12; ++c) X[c] = 0.0;
+        const int imm = mstep ? kDvBytes * (N - 1) : 2 * kDvBytes * t;  // this step's blocks
         if (act) {
-          const double* Si = DV + 78 * i;
+          if (!(mstep && g == 1)) {
 #pragma unroll
-          for (int c = 0; c < 12; ++c) Sr[c] = Si[offs[c]];
+            for (int c = 0; c < 12; ++c) Sr[c] = dv_at(DV, offs[c], imm);
+          }
           if (prev) {
             double V[12];
 #pragma unroll
@@ -464,9 +513,8 @@ struct RegCtx {
           // written twice with the two (rounding-different) halves of the symmetric inverse; the
           // later ds_write in program order wins, deterministically (shadow lanes 12..15 repeat row
           // 11 bit for bit). Cheaper than 12 per-element exec-masked stores.
-          double* Di = DV + 78 * i;
 #pragma unroll
-          for (int c = 0; c < 12; ++c) Di[offs[c]] = Dr[c];
+          for (int c = 0; c < 12; ++c) dv_at(DV, offs[c], imm) = Dr[c];
         }
       }
     }
@@ -554,11 +602,8 @@ struct RegCtx {
       const int cnt = g ? nb : nf;
       const double* cc = at(Lo::Cc) + 24 * g;
       CoupleRow Cr, Ct;  // row r of Cg and of Cg^T (compact layout, see the header)
-      int offs[12];
-#pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        offs[j] = sym_idx(pr, g ? perm12c(j) : j);
-      }
+      uint32_t offs[12];
+      load_chain_offs(lane, offs);
       Cr.d = cc[r];
       Cr.b = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
       Cr.a0 = r < 3 ? cc[12 + 3 * r] : 0.0;
@@ -583,10 +628,10 @@ struct RegCtx {
         double mv = 0.0;
         if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
         if (act && !(mstep && g == 1)) {
-          const double* Di = DV + 78 * i;
+          const int imm = mstep ? kDvBytes * (N - 1) : 2 * kDvBytes * t;
           double Dr[12];
 #pragma unroll
-          for (int k = 0; k < 12; ++k) Dr[k] = Di[offs[k]];
+          for (int k = 0; k < 12; ++k) Dr[k] = dv_at(DV, offs[k], imm);
           const double q = (QV[12 * i + pr] - cw) - mv;
           w = dot_bc12(Dr, q);
 #pragma unroll
@@ -597,20 +642,17 @@ struct RegCtx {
       const double ym = __shfl(w, perm12(r), 64);
       if (own && g == 0) QV[12 * mid + r] = w;
       double y = g ? ym : w;
+      // step te walks back from each group's last elimination step: both groups' blocks of step te
+      // sit at 1248 te, and w_te is register wv[te]
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int i = g ? mid + 1 + t : mid - 1 - t;
-        if (t < cnt) {
-          const int te = g ? N - 2 - mid - t : mid - 1 - t;  // elimination step of stage i
-          double wprev = 0.0;
-#pragma unroll
-          for (int k = 0; k <= T; ++k) wprev = (k == te) ? wv[k] : wprev;
-          const double* Di = DV + 78 * i;
+      for (int te = T - 1; te >= 0; --te) {
+        if (te < cnt) {
+          const int i = g ? N - 1 - te : te;
           double Dr[12];
 #pragma unroll
-          for (int k = 0; k < 12; ++k) Dr[k] = Di[offs[k]];
+          for (int k = 0; k < 12; ++k) Dr[k] = dv_at(DV, offs[k], 2 * kDvBytes * te);
           const double sc = couple_cty(Ct, y);  // Cg^T y_prev
-          y = wprev - dot_bc12(Dr, sc);
+          y = wv[te] - dot_bc12(Dr, sc);
           if (own) QV[12 * i + pr] = y;
         }
       }
