@@ -655,7 +655,7 @@ struct FastCtx {
 template <int NT>
 __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int env = blockIdx.x;
+  const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= args.batch) return;
   const int N = NT > 0 ? NT : args.N, lane = threadIdx.x;
   const FastLayout Lo(N);

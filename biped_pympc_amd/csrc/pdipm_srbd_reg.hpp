@@ -207,6 +207,21 @@ struct RegCtx {
   double* L;
   int lane;
   const double *fg, *hg, *bg;
+  // this lane's entries of f (x and u columns), b and h, held in registers for the whole solve:
+  // set once (loaded, or as the fused kernel computes them), never re-read from memory
+  double fxr[SX], fur[SX], bvr[SE], hvr[SI];
+  __device__ void load_qp_vectors() {
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {
+      const int c = min(lane + 64 * t, nx - 1);
+      fxr[t] = fg[c];
+      fur[t] = fg[nx + c];
+    }
+#pragma unroll
+    for (int t = 0; t < SE; ++t) bvr[t] = bg[min(lane + 64 * t, p - 1)];
+#pragma unroll
+    for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + 64 * t, m - 1)];
+  }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
   PROF_DECL
 
@@ -226,19 +241,7 @@ struct RegCtx {
     const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
                  *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
     double *RXu = at(Lo::RXu), *REm = at(Lo::REm);
-    // this lane's rows of f, h, b (global, L2-resident): all loads issued up front with clamped
-    // indices, so the phase waits for one L2 round trip instead of one per guarded chunk
-    double fx[SX], fu[SX], bv[SE], hv[SI];
-#pragma unroll
-    for (int t = 0; t < SX; ++t) {
-      const int c = min(lane + 64 * t, nx - 1);
-      fx[t] = fg[c];
-      fu[t] = fg[nx + c];
-    }
-#pragma unroll
-    for (int t = 0; t < SE; ++t) bv[t] = bg[min(lane + 64 * t, p - 1)];
-#pragma unroll
-    for (int t = 0; t < SI; ++t) hv[t] = hg[min(lane + 64 * t, m - 1)];
+    const double(&fx)[SX] = fxr, (&fu)[SX] = fur, (&bv)[SE] = bvr, (&hv)[SI] = hvr;
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
       const int c = lane + 64 * t;
@@ -749,7 +752,7 @@ template <int N, bool kFused>
 __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const FusedArgs& fa) {
   using Lo = RegLayout<N>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int env = blockIdx.x;
+  const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= (kFused ? fa.batch : args.batch)) return;
   const int lane = threadIdx.x;
   constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
@@ -814,6 +817,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.fg = fw;
     C.bg = bw;
     C.hg = dw;
+    C.load_qp_vectors();  // same lanes, same entries as written above: no other wave involved
   } else {
     const int nA = nnz_A(N), nG = 28 * N;
     const double* Hg = solver_in(args, 0) + (size_t)env * nz;
@@ -822,6 +826,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.fg = solver_in(args, 3) + (size_t)env * nz;
     C.hg = solver_in(args, 4) + (size_t)env * m;
     C.bg = solver_in(args, 5) + (size_t)env * p;
+    C.load_qp_vectors();
     // ---- compact load (stage 0/1 slices) ----
     for (int e = lane; e < 144; e += 64) {
       const int r = e / 12, j = e % 12;
@@ -928,7 +933,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     for (int t = 0; t < SI; ++t) {
       const int q = lane + 64 * t;
       if (q < m) {
-        C.s[t] = fmax(C.hg[q] - 0.0, 1.0);
+        C.s[t] = fmax(C.hvr[t] - 0.0, 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
       }

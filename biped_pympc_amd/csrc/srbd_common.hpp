@@ -173,6 +173,16 @@ constexpr Tables make_tables() {
   return t;
 }
 
+// XCD-aware block -> work-item map. Workgroups are dealt round-robin over the 8 XCDs (block b on
+// XCD b % 8; MI355X_MICROARCH.md, workgroup dispatch), and each XCD has its own L2: give XCD x one
+// CONTIGUOUS range of items, so the 128-byte lines of the small per-env input rows (dt, m, mu,
+// R_body, feet, ... 8-96 B each) are fetched by one L2 instead of up to eight. Placement is a speed
+// hint only: the map is a bijection on [0, G), so results never depend on it.
+__device__ __forceinline__ int xcd_item(int b, int G) {
+  const int x = b & 7, q = G >> 3, r = G & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // Pattern tables in constant memory (one translation unit: srbd_mpc.hip).
 static __constant__ Tables c_tab = make_tables();
 
