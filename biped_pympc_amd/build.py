@@ -76,8 +76,8 @@ def build_dropin(kind: str, N: int, K: int | None) -> str:
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     core = os.path.join(LIB_DIR, "libsrbd_mpc.so")
-    srcs = [os.path.join(CSRC, f) for f in
-            ("srbd_mpc.hip", "srbd_common.hpp", "pdipm.hpp", "qp_former.hpp")]
+    # the translation unit and every header it includes (csrc/*.hpp)
+    srcs = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))]
     srcs.append(os.path.join(INCLUDE, "srbd_mpc.h"))
     if force or not _newer(core, srcs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

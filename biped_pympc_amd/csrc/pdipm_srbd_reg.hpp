@@ -25,15 +25,23 @@
 
 namespace srbd {
 
-template <int N>
+// Threads per QP: one wave at N <= 10 (LDS and registers allow 2 QPs per SIMD); two waves beyond
+// (the LDS of a longer horizon allows 1 QP per SIMD, so a second wave of the SAME QP takes the other
+// half of every row-parallel phase and gives the SIMD a partner to hide latency behind). The block
+// chains and the per-stage tasks stay on wave 0.
+__host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : 128; }
+
+template <int N, int TPB = reg_tpb(N)>
 struct RegLayout {
   static constexpr int nz = 24 * N, m = 16 * N, p = 14 * N, nx = 12 * N;
   static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 144, K0 = Gf + 64, K1 = K0 + 78,
                        Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, TRI = SG + 16,
                        DV = TRI + 10,
                        X = DV + 78 * N, Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
-                       QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N, total = DYm + 2 * N;
-  static constexpr int SI = (m + 63) / 64, SE = (p + 63) / 64, SX = (nx + 63) / 64;
+                       QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
+                       RED = DYm + 2 * N,  // block reductions of a 2-wave QP: 2 slot pairs
+                       total = RED + (TPB > 64 ? 4 : 0);
+  static constexpr int SI = (m + TPB - 1) / TPB, SE = (p + TPB - 1) / TPB, SX = (nx + TPB - 1) / TPB;
   static_assert((DV & 1) == 0 && (X & 1) == 0 && (TV & 1) == 0, "16-byte aligned vectors");
 };
 
@@ -199,6 +207,7 @@ __device__ __forceinline__ double grow4(const double* gf, int k, const double* x
 
 template <int N>
 struct RegCtx {
+  static constexpr int TPB = reg_tpb(N);
   using Lo = RegLayout<N>;
   static constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx;
   static constexpr int SI = Lo::SI, SE = Lo::SE, SX = Lo::SX;
@@ -213,19 +222,38 @@ struct RegCtx {
   __device__ void load_qp_vectors() {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
-      const int c = min(lane + 64 * t, nx - 1);
+      const int c = min(lane + TPB * t, nx - 1);
       fxr[t] = fg[c];
       fur[t] = fg[nx + c];
     }
 #pragma unroll
-    for (int t = 0; t < SE; ++t) bvr[t] = bg[min(lane + 64 * t, p - 1)];
+    for (int t = 0; t < SE; ++t) bvr[t] = bg[min(lane + TPB * t, p - 1)];
 #pragma unroll
-    for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + 64 * t, m - 1)];
+    for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
   PROF_DECL
 
   __device__ double* at(int off) const { return L + off; }
+  // Sum / min over the QP's threads. One wave: a DPP wave reduction. Two waves: each wave reduces,
+  // writes its partial to LDS, and after a barrier both combine the partials in the same order
+  // (identical result in both waves). Consecutive reductions alternate slot pairs: a wave writes
+  // pair k only after passing reduction k-1's barrier, i.e. after the other wave has read pair k.
+  int red_k = 0;
+  template <bool kMin>
+  __device__ double block_reduce(double v) {
+    v = kMin ? wave_min(v) : wave_sum(v);
+    if constexpr (TPB > 64) {
+      double* R = at(Lo::RED) + 2 * red_k;
+      red_k ^= 1;
+      if ((lane & 63) == 0) R[lane >> 6] = v;
+      __syncthreads();
+      v = kMin ? fmin(R[0], R[1]) : R[0] + R[1];
+    }
+    return v;
+  }
+  __device__ double block_sum(double v) { return block_reduce<false>(v); }
+  __device__ double block_min(double v) { return block_reduce<true>(v); }
   // The lane index, re-materialised as an opaque value at the start of every phase: keeps the
   // compiler from hoisting each phase's per-lane addresses and predicates out of the Newton loop
   // (that alone pinned > 100 registers for the whole solve).
@@ -244,7 +272,7 @@ struct RegCtx {
     const double(&fx)[SX] = fxr, (&fu)[SX] = fur, (&bv)[SE] = bvr, (&hv)[SI] = hvr;
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
-      const int c = lane + 64 * t;
+      const int c = lane + TPB * t;
       if (c < nx) {
         const int k = c / 12 + 1, j = c % 12;
         const double v = Hu[12 + j] * X[c] + fx[t];
@@ -255,7 +283,7 @@ struct RegCtx {
     }
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, u columns: H_u u + f + G^T z + N^T y + e-rows (LDS)
-      const int c = lane + 64 * t;
+      const int c = lane + TPB * t;
       if (c < nx) {
         const int i = c / 12, j = c % 12;
         const double v = Hu[j] * X[nx + c] + fu[t];
@@ -281,7 +309,7 @@ struct RegCtx {
     }
 #pragma unroll
     for (int t = 0; t < SE; ++t) {  // r_e = A x - b (owner regs; x-moment rows also in LDS)
-      const int e = lane + 64 * t;
+      const int e = lane + TPB * t;
       if (e < p) {
         double v;
         if (e < nx) {
@@ -300,7 +328,7 @@ struct RegCtx {
     double sz = 0.0;
 #pragma unroll
     for (int t = 0; t < SI; ++t) {  // r_s = G u + s - h (owner regs)
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         const int i = q / 16, k = q % 16;
         const double v = grow4(Gf, k, X + nx + 12 * i);
@@ -309,7 +337,7 @@ struct RegCtx {
       }
     }
     __syncthreads();
-    return wave_sum(sz) / m;
+    return block_sum(sz) / m;
   }
 
   // -------------------------------------------------------------------- factorise ----
@@ -326,7 +354,7 @@ struct RegCtx {
     const uint8_t* TRI = reinterpret_cast<const uint8_t*>(at(Lo::TRI));
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         wd[t] = rcp3(s[t]) * z[t] + kDelta;  // correctly rounded reciprocals (rcp3), not IEEE division
         di[t] = rcp3(1.0 + kDelta * wd[t]);
@@ -535,7 +563,7 @@ struct RegCtx {
                  *DV = at(Lo::DV);
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         const double si = rcp3(s[t]);
         double r2 = -(si * (s[t] * z[t]));
@@ -545,7 +573,7 @@ struct RegCtx {
     }
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
-      const int c = lane + 64 * t;
+      const int c = lane + TPB * t;
       if (c < nx) TV[c] = -rxx[t] * IX[c % 12];
     }
     __syncthreads();
@@ -585,7 +613,7 @@ struct RegCtx {
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < SE; ++t) {  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
-      const int e = lane + 64 * t;
+      const int e = lane + TPB * t;
       if (e < nx) {
         const int i = e / 12, r = e % 12;
         double v = (i >= 1) ? mrow(Mc, r, TV + 12 * (i - 1)) : 0.0;
@@ -664,7 +692,7 @@ struct RegCtx {
     PROF_ADD(4);
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
-      const int c = lane + 64 * t;
+      const int c = lane + TPB * t;
       if (c < nx) {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
@@ -706,7 +734,7 @@ struct RegCtx {
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < SI; ++t) {  // dz, ds (owner regs)
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         const int i = q / 16, k = q % 16;
         const double gd = grow4(Gf, k, TV + nx + 12 * i);
@@ -717,19 +745,19 @@ struct RegCtx {
     PROF_ADD(3);
   }
 
-  __device__ double step_length(const double (&v)[SI], const double (&dv)[SI]) const {
+  __device__ double step_length(const double (&v)[SI], const double (&dv)[SI]) {
     const int lane = fresh_lane();
     double mn = INFINITY;
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         const bool c = dv[t] < 0.0;
         const double a = -v[t] * rcp3(dv[t]);
         mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
       }
     }
-    mn = wave_min(mn);
+    mn = block_min(mn);
     return fmax(fmin(1.0, 0.99 * mn), 1e-12);
   }
 };
@@ -751,6 +779,7 @@ struct FusedArgs {
 template <int N, bool kFused>
 __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const FusedArgs& fa) {
   using Lo = RegLayout<N>;
+  constexpr int TPB = reg_tpb(N);
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= (kFused ? fa.batch : args.batch)) return;
@@ -775,13 +804,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     for (int i = 0; i < 17; ++i) P[i] = fa.in[i] + (size_t)env * in_nnz[i];
     former_model(F, P, lane);
     const double mu = P[6][0];
-    for (int e = lane; e < 144; e += 64) {
+    for (int e = lane; e < 144; e += TPB) {
       const int r = e / 12, j = e % 12;
       const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
       Md[e] = (N >= 2 && om >= 0) ? F.XB[om] : 0.0;
       Nd[e] = on >= 0 ? F.UB[on] : 0.0;
     }
-    Gf[lane] = 0.0;  // 64 entries
+    if (lane < 64) Gf[lane] = 0.0;  // 64 entries
     if (lane < 12) {
       Pd[lane] = F.XB[c_tab.cpx[lane]];
       Hu[lane] = P[14][lane];       // H = diag(Q.., R..): u part R
@@ -799,7 +828,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     double* dw = fa.vec[2] + (size_t)env * m;
 #pragma unroll
     for (int t = 0; t < Lo::SX; ++t) {
-      const int c = lane + 64 * t;
+      const int c = lane + TPB * t;
       if (c < nx) {
         fw[c] = former_f(c, N, P[13], P[14], P[1], P[2], P[3]);
         fw[nx + c] = former_f(nx + c, N, P[13], P[14], P[1], P[2], P[3]);
@@ -807,10 +836,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
 #pragma unroll
     for (int t = 0; t < Lo::SE; ++t)
-      if (lane + 64 * t < p) bw[lane + 64 * t] = former_b(lane + 64 * t, N, F);
+      if (lane + TPB * t < p) bw[lane + TPB * t] = former_b(lane + TPB * t, N, F);
 #pragma unroll
     for (int t = 0; t < SI; ++t)
-      if (lane + 64 * t < m) dw[lane + 64 * t] = former_d(lane + 64 * t, N, P[2], P[12], mu);
+      if (lane + TPB * t < m) dw[lane + TPB * t] = former_d(lane + TPB * t, N, P[2], P[12], mu);
     // each entry is re-read only by the lane that wrote it: workgroup scope orders that (a device-
     // scope release would write back L2)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -828,13 +857,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.bg = solver_in(args, 5) + (size_t)env * p;
     C.load_qp_vectors();
     // ---- compact load (stage 0/1 slices) ----
-    for (int e = lane; e < 144; e += 64) {
+    for (int e = lane; e < 144; e += TPB) {
       const int r = e / 12, j = e % 12;
       const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
       Md[e] = (N >= 2 && om >= 0) ? Ag[a_xblock(1) + om] : 0.0;
       Nd[e] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
     }
-    Gf[lane] = 0.0;  // 64 entries
+    if (lane < 64) Gf[lane] = 0.0;  // 64 entries
     if (lane < 12) {
       Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
       Hu[lane] = Hg[nx + lane];
@@ -850,22 +879,29 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     // x_k blocks (36 values, k = 1..N-1) vs x_1's; the x_N single entries vs x_1's +I entries (P);
     // u_i blocks (86 values) vs u_0's (the latter include the x-moment entries e6/e9)
     bool bad = false;
-    for (int e = lane; e < nA; e += 64) {
+    for (int e = lane; e < nA; e += TPB) {
       int ref;
       if (e < 36 * (N - 1)) ref = e % 36;
       else if (e < a_ubase(N)) ref = c_tab.cpx[e - 36 * (N - 1)];
       else ref = a_ubase(N) + (e - a_ubase(N)) % 86;
       bad |= !(Ag[e] == Ag[ref]);
     }
-    for (int e = lane; e < nG; e += 64) bad |= !(Gg[e] == Gg[e % 28]);
-    for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
-    if (__any(bad)) {
+    for (int e = lane; e < nG; e += TPB) bad |= !(Gg[e] == Gg[e % 28]);
+    for (int e = lane; e < nz; e += TPB) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
+    bad = __any(bad);
+    if constexpr (TPB > 64) {  // one verdict for the whole QP (both waves leave or both stay)
+      if ((lane & 63) == 0) reinterpret_cast<int*>(smem + Lo::RED)[lane >> 6] = bad;
+      __syncthreads();
+      bad = reinterpret_cast<int*>(smem + Lo::RED)[0] | reinterpret_cast<int*>(smem + Lo::RED)[1];
+      __syncthreads();  // RED is reused by the first block reduction
+    }
+    if (bad) {
       if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
       return;
     }
   }
   // ---- per-QP constants ----
-  for (int l = lane; l < 78; l += 64) reinterpret_cast<uint8_t*>(smem + Lo::TRI)[l] = c_tab.dvo[l];
+  for (int l = lane; l < 78; l += TPB) reinterpret_cast<uint8_t*>(smem + Lo::TRI)[l] = c_tab.dvo[l];
   if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
   if (lane == 0) {
     const double p6 = Hu[6] + kBeta, p9 = Hu[9] + kBeta;
@@ -897,7 +933,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     else l1 = lane;
     Cc[24 + l1] = cv;
   }
-  for (int e = lane; e < 78; e += 64) {
+  for (int e = lane; e < 78; e += TPB) {
     int r, c;
     tri_rc(e, r, c);
     double k0 = (r == c) ? Pd[r] * Pd[r] * IX[r] + kDelta : 0.0;
@@ -910,35 +946,38 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     K1[e] = k1;
   }
   // ---- iterate ----
+  // X aliases the dense M the K0 / K1 loop above reads: with two waves, the other wave must be past
+  // that loop before X is written (one wave runs both loops in order)
+  if constexpr (TPB > 64) __syncthreads();
   double *X = smem + Lo::X, *Z = smem + Lo::Z, *Y = smem + Lo::Y;
   if (!kFused && args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;
     const double* yg = solver_in(args, 9) + (size_t)env * p;
-    for (int e = lane; e < nz; e += 64) X[e] = xg[e];
+    for (int e = lane; e < nz; e += TPB) X[e] = xg[e];
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         C.s[t] = sg[q];
         C.z[t] = zg[q];
         Z[q] = C.z[t];
       }
     }
-    for (int e = lane; e < p; e += 64) Y[e] = yg[e];
+    for (int e = lane; e < p; e += TPB) Y[e] = yg[e];
   } else {
-    for (int e = lane; e < nz; e += 64) X[e] = 0.0;
+    for (int e = lane; e < nz; e += TPB) X[e] = 0.0;
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = lane + 64 * t;
+      const int q = lane + TPB * t;
       if (q < m) {
         C.s[t] = fmax(C.hvr[t] - 0.0, 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
       }
     }
-    for (int e = lane; e < p; e += 64) Y[e] = kFused ? fa.y0 : args.y0;
+    for (int e = lane; e < p; e += TPB) Y[e] = kFused ? fa.y0 : args.y0;
   }
   __syncthreads();
 
@@ -970,8 +1009,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     int ul = C.fresh_lane();
 #pragma unroll
     for (int t = 0; t < SI; ++t)
-      if (ul + 64 * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
-    const double mu_aff = wave_sum(sza) / m;
+      if (ul + TPB * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
+    const double mu_aff = C.block_sum(sza) / m;
     const double ratio = mu_aff / mu;
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
     __syncthreads();
@@ -981,10 +1020,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     __syncthreads();
     double szn = 0.0;
     ul = C.fresh_lane();
-    for (int e = ul; e < nz; e += 64) X[e] = X[e] + apc * TV[e];
+    for (int e = ul; e < nz; e += TPB) X[e] = X[e] + apc * TV[e];
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
-      const int q = ul + 64 * t;
+      const int q = ul + TPB * t;
       if (q < m) {
         const double sn = fmax(C.s[t] + apc * C.ds[t], 1e-8);
         const double zn = fmax(fmax(C.z[t] + adc * C.dz[t], 1e-8), 1e-8);
@@ -994,22 +1033,22 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         szn += sn * zn;
       }
     }
-    for (int e = ul; e < p; e += 64) Y[e] = Y[e] + adc * (e < nx ? QV[e] : DYm[e - nx]);
-    mu_new = wave_sum(szn) / m;
+    for (int e = ul; e < p; e += TPB) Y[e] = Y[e] + adc * (e < nx ? QV[e] : DYm[e - nx]);
+    mu_new = C.block_sum(szn) / m;
     if (it == n_iter - 1) {
       double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
       for (int t = 0; t < Lo::SX; ++t)
-        if (ul + 64 * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + 64 * t] * RXu[ul + 64 * t];
+        if (ul + TPB * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + TPB * t] * RXu[ul + TPB * t];
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (ul + 64 * t < m) b += C.rs[t] * C.rs[t];
+        if (ul + TPB * t < m) b += C.rs[t] * C.rs[t];
 #pragma unroll
       for (int t = 0; t < Lo::SE; ++t)
-        if (ul + 64 * t < p) c += C.re[t] * C.re[t];
-      res0 = sqrt(wave_sum(a));
-      res1 = sqrt(wave_sum(b));
-      res2 = sqrt(wave_sum(c));
+        if (ul + TPB * t < p) c += C.re[t] * C.re[t];
+      res0 = sqrt(C.block_sum(a));
+      res1 = sqrt(C.block_sum(b));
+      res2 = sqrt(C.block_sum(c));
     }
     __syncthreads();
     PROF_ADD_CTX(C, 5);
@@ -1022,16 +1061,16 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   double* yo = outp(3) + (size_t)env * p;
   double* ro = outp(4) + (size_t)env * 4;
   double* mo = outp(5) + (size_t)env;
-  for (int e = lane; e < nz; e += 64) xo[e] = X[e];
+  for (int e = lane; e < nz; e += TPB) xo[e] = X[e];
 #pragma unroll
   for (int t = 0; t < SI; ++t) {
-    const int q = lane + 64 * t;
+    const int q = lane + TPB * t;
     if (q < m) {
       so[q] = C.s[t];
       zo[q] = C.z[t];
     }
   }
-  for (int e = lane; e < p; e += 64) yo[e] = Y[e];
+  for (int e = lane; e < p; e += TPB) yo[e] = Y[e];
   if (lane == 0) {
     ro[0] = res0;
     ro[1] = res1;
@@ -1041,14 +1080,14 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   }
 }
 
-// N <= 10: 2 waves per SIMD (<= 256 registers); longer horizons: LDS allows 1 wave per SIMD anyway
+// 2 waves per SIMD: 2 one-wave QPs (N <= 10) or 1 two-wave QP (N = 20) per SIMD, <= 256 registers
 template <int N>
-__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void pdipm_srbd_reg_kernel(SolverArgs args) {
+__global__ __launch_bounds__(reg_tpb(N), 2) void pdipm_srbd_reg_kernel(SolverArgs args) {
   reg_kernel_body<N, false>(args, FusedArgs{});
 }
 
 template <int N>
-__global__ __launch_bounds__(64, (N <= 10 ? 2 : 1)) void mpc_step_reg_kernel(FusedArgs fa) {
+__global__ __launch_bounds__(reg_tpb(N), 2) void mpc_step_reg_kernel(FusedArgs fa) {
   reg_kernel_body<N, true>(SolverArgs{}, fa);
 }
 

@@ -72,7 +72,7 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
       hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
     } else {
       if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, &cfg_reg20)) return rc;
-      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(64), kRegLds20, s, a);
+      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, s, a);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
@@ -292,7 +292,7 @@ int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const do
     hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(batch), dim3(64), kRegLds10, st, a);
   } else {
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, &cfg20)) return rc;
-    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(batch), dim3(64), kRegLds20, st, a);
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(batch), dim3(srbd::reg_tpb(20)), kRegLds20, st, a);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ SQ_IFETCH SQ_WAVES -d gpurun_out/icache -o run --output-format csv -- \
-  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 > /dev/null 2> gpurun_out/icache.err || exit 1
+  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 "$@" > /dev/null 2> gpurun_out/icache.err || exit 1
 python3 - <<'PY' > gpurun_out/icache.txt
 import csv, glob
 acc = {}

@@ -14,7 +14,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "pdipm_srbd_reg_kernel<10>"
+HORIZON = os.environ.get("VC_N", "10")  # horizon of the measured solver kernel
+KERNEL = f"pdipm_srbd_reg_kernel<{HORIZON}>"
 COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAVE_CYCLES"]
 
 
@@ -29,7 +30,7 @@ def main():
                         *flags.split(), "-I", os.path.join(ROOT, "include"), "-o", lib,
                         os.path.join(csrc, "srbd_mpc.hip")], check=True)
         env = {**os.environ, "SRBD_LIB": lib}
-        cmd = [sys.executable, os.path.join(ROOT, "scripts/kernel_ab.py"), "10", "4096", "10", "auto"]
+        cmd = [sys.executable, os.path.join(ROOT, "scripts/kernel_ab.py"), HORIZON, "4096", "10", "auto"]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             raise SystemExit(f"{name}: kernel_ab failed\n{r.stdout}\n{r.stderr}")
@@ -45,7 +46,7 @@ def main():
                 for row in csv.DictReader(fh):
                     if KERNEL in row["Kernel_Name"] and row["Counter_Name"] in acc:
                         acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
-                        waves = int(row["Grid_Size"]) // 64
+                        waves = int(row["Grid_Size"]) // 64  # per wave (a 2-wave QP counts twice)
         vals = {c: (sum(v) / len(v) / waves if v else float("nan")) for c, v in acc.items()}
         rows.append((name, flags, ms, vals))
         print(f"{name:12s} {ms:8.4f} ms  " + "  ".join(f"{c[3:]} {vals[c]:9.0f}" for c in COUNTERS)
