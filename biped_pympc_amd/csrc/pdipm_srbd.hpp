@@ -153,6 +153,17 @@ __device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc
 #else
   const double pk = bc16(Sr[K], K);
 #endif
+#ifdef SRBD_GJ_SELECT  // pivot-lane special cases as selects on a lane compare (no EXEC writes)
+  const int l16 = __lane_id() & 15;
+  const bool piv = K == 11 ? l16 >= 11 : l16 == K;
+  Sr[K] = piv ? 0.0 : Sr[K];
+  const double id = rcp3(pk);
+  const double t = Sr[K] * id;  // 0 on the pivot lanes
+  pivot_update(Sr, t, K);
+  Sr[K] = piv ? -1.0 : t;
+  sc = piv ? id : sc;
+  if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
+#else
   uint64_t sv;
   asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], 0\n\ts_mov_b64 exec, %[sv]"
       : [x] "+v"(Sr[K]), [sv] "=&s"(sv)
@@ -169,6 +180,7 @@ __device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc
 #else
   if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
 #endif
+#endif  // SRBD_GJ_SELECT
 }
 
 __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], double (&Dr)[12]) {

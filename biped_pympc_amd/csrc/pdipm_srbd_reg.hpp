@@ -212,7 +212,7 @@ struct RegCtx {
   static constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx;
   static constexpr int SI = Lo::SI, SE = Lo::SE, SX = Lo::SX;
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
-  static constexpr int kFactorUnroll = N <= 10 ? T + 1 : 1;
+  static constexpr int kFactorUnroll = T + 1;  // chains fully unrolled (N = 20: -4.7 % vs rolled)
   double* L;
   int lane;
   const double *fg, *hg, *bg;
@@ -394,8 +394,12 @@ struct RegCtx {
     // touching rows {3,4,5,9,10,11} of N needs 10 FMAs instead of 40
     // Each lane keeps ONE entry (r, c) for the whole pass, so its table entry, N rows and K values
     // are loaded once; only Phi_f^-1 (PHs) changes with the stage.
-    if (lane < 63) {  // dense x dense: lane = 21 q + k -> entry k of stages 3 t + q
-      const int q = lane / 21, k = lane - 21 * q;
+    // with two waves each takes half of the stages: wave w's lane l < 63 -> class q = 3 w + l / 21
+    constexpr int NW = TPB / 64, NQ = 3 * NW;
+    static_assert(N % NW == 0, "stages split evenly over the waves");
+    const int lw = lane & 63, wv = lane >> 6;
+    if (lw < 63) {  // dense x dense: lw = 21 q' + k -> entry k of stages NQ t + q, q = 3 wv + q'
+      const int q = 3 * wv + lw / 21, k = lw - 21 * (lw / 21);
       const int rc = TRI[k], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
       double vr[2][4], vc[2][4];
 #pragma unroll
@@ -407,8 +411,8 @@ struct RegCtx {
         }
       const double k0 = K0[sy], k1 = K1[sy];
 #pragma unroll
-      for (int t = 0; t < (N + 2) / 3; ++t) {
-        const int i = 3 * t + q;
+      for (int t = 0; t < (N + NQ - 1) / NQ; ++t) {
+        const int i = NQ * t + q;
         if (i < N) {
           double v = i == 0 ? k0 : k1;
 #pragma unroll
@@ -426,10 +430,10 @@ struct RegCtx {
         }
       }
     }
-    if (lane < 57) {  // the 57 entries with a sparse index (rows {3,4,5,9,10,11} of N hold one entry
+    if (lw < 57) {  // the 57 entries with a sparse index (rows {3,4,5,9,10,11} of N hold one entry
                       // per foot, at position r % 3), one stage per trip; for a sparse x sparse entry
                       // the 4-term sum over the "dense" index meets N's zeros, so it is exact too
-      const int rc = TRI[21 + lane], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
+      const int rc = TRI[21 + lw], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
       const bool rs = (r % 6) >= 3;
       const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
       double nd[2][4], ns[2];
@@ -444,7 +448,7 @@ struct RegCtx {
       for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
       const double k0 = K0[sy], k1 = K1[sy];
 #pragma unroll 2
-      for (int i = 0; i < N; ++i) {
+      for (int i = wv * (N / NW); i < (wv + 1) * (N / NW); ++i) {  // wave wv's share of the stages
         double v = i == 0 ? k0 : k1;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
@@ -482,10 +486,16 @@ struct RegCtx {
       const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
       uint32_t offs[12];  // byte offset of (pr, column c in group coordinates) in a step's blocks
       load_chain_offs(lane, offs);
+#ifdef SRBD_EXP_CCREG  // experiment: the group's 24 coupling values in registers for the whole chain
+      double ccv[24];
+#pragma unroll
+      for (int k = 0; k < 24; ++k) ccv[k] = cc[k];
+#else
+      const double* ccv = cc;
+#endif
       double Dr[12];
 #pragma unroll
       for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
-      // fully unrolled at N = 10 (measured 1.5 % faster); the 11-step N = 20 chain stays rolled
 #pragma unroll kFactorUnroll
       for (int t = 0; t <= T; ++t) {
         const bool mstep = (t == T);
@@ -501,13 +511,17 @@ struct RegCtx {
 #pragma unroll
             for (int c = 0; c < 12; ++c) Sr[c] = dv_at(DV, offs[c], imm);
           }
+#ifdef SRBD_EXP_NOSCHUR  // timing experiment only (wrong results): no Schur update
+          if (false) {
+#else
           if (prev) {
+#endif
             double V[12];
 #pragma unroll
             for (int c = 0; c < 12; ++c) {
-              double v = Dr[c] * cc[c];
-              if (c < 3) v += (Dr[6] * cc[12 + 3 * c] + Dr[7] * cc[13 + 3 * c]) + Dr[8] * cc[14 + 3 * c];
-              else if (c < 6) v += Dr[c + 6] * cc[21 + c - 3];
+              double v = Dr[c] * ccv[c];
+              if (c < 3) v += (Dr[6] * ccv[12 + 3 * c] + Dr[7] * ccv[13 + 3 * c]) + Dr[8] * ccv[14 + 3 * c];
+              else if (c < 6) v += Dr[c + 6] * ccv[21 + c - 3];
               V[c] = v;
             }
             if (!mstep) {  // S - X accumulated in place
@@ -539,7 +553,12 @@ struct RegCtx {
           }
         }
         if (act && !(mstep && g == 1)) {
+#ifdef SRBD_EXP_NOINV  // timing experiment only (wrong results): no block inverse
+#pragma unroll
+          for (int c = 0; c < 12; ++c) Dr[c] = Sr[c];
+#else
           inverse_rows12(Sr, Dr);
+#endif
           // every lane writes its whole row: (r, c) and (c, r) share a packed slot, so each slot is
           // written twice with the two (rounding-different) halves of the symmetric inverse; the
           // later ds_write in program order wins, deterministically (shadow lanes 12..15 repeat row
