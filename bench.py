@@ -96,11 +96,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal hooks for the N > 1 path on a one-GPU box (never set by the driver): all ranks on
+    # device 0, and gloo instead of RCCL (RCCL rejects two ranks on one device)
+    one_device = os.environ.get("SRBD_BENCH_ONE_DEVICE") == "1"
+    backend = os.environ.get("SRBD_BENCH_BACKEND", "nccl")
+    if one_device:
+        local = 0
     if world > 1:
         import torch.distributed as dist_mod
         dist = dist_mod
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
     N, K, B = a.horizon, a.iters, a.batch_per_gpu
@@ -226,7 +235,8 @@ def main():
                                    + (", randomized gait" if a.random_gait else ", standing gait"),
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
                        "pdipm_iters": K, "qp_dims": [d.nz, d.n_eq, d.n_ineq],
-                       "parallelism": f"dp{world}" + (" (u0 all_gather over RCCL)" if world > 1 else "")},
+                       "parallelism": f"dp{world}" + (f" (u0 all_gather over {'RCCL' if backend == 'nccl' else backend})"
+                                                      if world > 1 else "")},
             "kernels_ms": {"mpc_step_fused": round(ms_fused, 4) if fused else None,
                            "qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
                            "u0_all_gather": None if ms_gather is None else round(ms_gather, 4)},
