@@ -178,10 +178,22 @@ constexpr Tables make_tables() {
 // CONTIGUOUS range of items, so the 128-byte lines of the small per-env input rows (dt, m, mu,
 // R_body, feet, ... 8-96 B each) are fetched by one L2 instead of up to eight. Placement is a speed
 // hint only: the map is a bijection on [0, G), so results never depend on it.
-__device__ __forceinline__ int xcd_item(int b, int G) {
+__host__ __device__ constexpr int xcd_item(int b, int G) {
   const int x = b & 7, q = G >> 3, r = G & 7;
   return x * q + (x < r ? x : r) + (b >> 3);
 }
+constexpr bool xcd_item_is_bijection(int G) {  // every item hit exactly once
+  unsigned long long seen[8] = {};
+  for (int b = 0; b < G; ++b) {
+    const int e = xcd_item(b, G);
+    if (e < 0 || e >= G || (seen[e >> 6] >> (e & 63) & 1)) return false;
+    seen[e >> 6] |= 1ull << (e & 63);
+  }
+  return true;
+}
+static_assert(xcd_item_is_bijection(1) && xcd_item_is_bijection(7) && xcd_item_is_bijection(8) &&
+                  xcd_item_is_bijection(13) && xcd_item_is_bijection(64) && xcd_item_is_bijection(509),
+              "xcd_item must permute [0, G)");
 
 // Pattern tables in constant memory (one translation unit: srbd_mpc.hip).
 static __constant__ Tables c_tab = make_tables();
