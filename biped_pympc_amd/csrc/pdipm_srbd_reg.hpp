@@ -211,6 +211,40 @@ struct RegCtx {
   using Lo = RegLayout<N>;
   static constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx;
   static constexpr int SI = Lo::SI, SE = Lo::SE, SX = Lo::SX;
+  // Equality rows by register slot: slot 0 holds the dynamics rows {0,1,2,6,7,8} of every stage (the
+  // dense rows of the u-block N), slot 1 rows {3,4,5,9,10,11} (two force columns each), slot 2 the
+  // x-moment rows, so each slot's row formula is the same in every lane.
+  static_assert(SE == 3 && 6 * N <= TPB && 2 * N <= TPB, "equality-row slots");
+  struct ERow {
+    int e, i, r;
+    bool valid;
+  };
+  __device__ static ERow erow(int l, int t) {
+    ERow q;
+    if (t == 2) {
+      q.valid = l < 2 * N;
+      q.e = nx + l;
+      q.i = l >> 1;
+      q.r = l & 1;
+      return q;
+    }
+    q.valid = l < 6 * N;
+    q.i = l / 6;
+    const int k = l - 6 * q.i;
+    q.r = t == 0 ? (k < 3 ? k : k + 3) : (k < 3 ? k + 3 : k + 6);
+    q.e = 12 * q.i + q.r;
+    return q;
+  }
+  // (N u)_r of stage i's u block for a slot-t row (slot 1: the two force columns of row r)
+  template <int t>
+  __device__ static double nrow(const double* nd, int r, const double* u) {
+    if constexpr (t == 0) {
+      return drow12(nd + 12 * r, u);
+    } else {
+      const int p = r % 3;
+      return nd[12 * r + p] * u[p] + nd[12 * r + 3 + p] * u[3 + p];
+    }
+  }
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
   static constexpr int kFactorUnroll = T + 1;  // chains fully unrolled (N = 20: -4.7 % vs rolled)
   double* L;
@@ -227,7 +261,10 @@ struct RegCtx {
       fur[t] = fg[nx + c];
     }
 #pragma unroll
-    for (int t = 0; t < SE; ++t) bvr[t] = bg[min(lane + TPB * t, p - 1)];
+    for (int t = 0; t < SE; ++t) {
+      const ERow q = erow(lane, t);
+      bvr[t] = bg[q.valid ? q.e : 0];
+    }
 #pragma unroll
     for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
@@ -264,6 +301,27 @@ struct RegCtx {
   }
 
   // --------------------------------------------------------------------- residuals ----
+  template <int t>
+  __device__ void re_slot(const double* X, const double* Mc, const double* Pd, const double* Nd,
+                          const double (&bv)[SE]) {
+    const ERow q = erow(fresh_lane(), t);
+    if (q.valid) {
+      double v = (q.i >= 1) ? mrow(Mc, q.r, X + 12 * (q.i - 1)) : 0.0;
+      v += Pd[q.r] * X[12 * q.i + q.r];
+      v += nrow<t>(Nd, q.r, X + nx + 12 * q.i);
+      re[t] = v - bv[t];
+    }
+  }
+  template <int t>
+  __device__ void g_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV) {
+    const ERow q = erow(fresh_lane(), t);
+    if (q.valid) {
+      double v = (q.i >= 1) ? mrow(Mc, q.r, TV + 12 * (q.i - 1)) : 0.0;
+      v += Pd[q.r] * TV[12 * q.i + q.r];
+      v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
+      QV[q.e] = v + re[t];
+    }
+  }
   SRBD_PHASE_ATTR __device__ double residuals() {
     const int lane = fresh_lane();
     const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
@@ -307,22 +365,14 @@ struct RegCtx {
         RXu[c] = (v + gz) + ay;
       }
     }
-#pragma unroll
-    for (int t = 0; t < SE; ++t) {  // r_e = A x - b (owner regs; x-moment rows also in LDS)
-      const int e = lane + TPB * t;
-      if (e < p) {
-        double v;
-        if (e < nx) {
-          const int i = e / 12, r = e % 12;
-          v = (i >= 1) ? mrow(Mc, r, X + 12 * (i - 1)) : 0.0;
-          v += Pd[r] * X[12 * i + r];
-          v += drow12(Nd + 12 * r, X + nx + 12 * i);
-        } else {
-          const int i = (e - nx) / 2, w = (e - nx) % 2;
-          v = SG[6 + w] * X[nx + 12 * i + (w ? 9 : 6)];
-        }
-        re[t] = v - bv[t];
-        if (e >= nx) REm[e - nx] = re[t];
+    re_slot<0>(X, Mc, Pd, Nd, bv);  // r_e = A x - b (owner regs; x-moment rows also in LDS)
+    re_slot<1>(X, Mc, Pd, Nd, bv);
+    {
+      const ERow q = erow(lane, 2);
+      if (q.valid) {
+        const int w = q.r;
+        re[2] = SG[6 + w] * X[nx + 12 * q.i + (w ? 9 : 6)] - bv[2];
+        REm[q.e - nx] = re[2];
       }
     }
     double sz = 0.0;
@@ -630,17 +680,8 @@ struct RegCtx {
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int t = 0; t < SE; ++t) {  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
-      const int e = lane + TPB * t;
-      if (e < nx) {
-        const int i = e / 12, r = e % 12;
-        double v = (i >= 1) ? mrow(Mc, r, TV + 12 * (i - 1)) : 0.0;
-        v += Pd[r] * TV[12 * i + r];
-        v += drow12(Nd + 12 * r, TV + nx + 12 * i);
-        QV[e] = v + re[t];
-      }
-    }
+    g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
+    g_slot<1>(TV, Mc, Pd, Nd, QV);
     __syncthreads();
     PROF_ADD(3);
     // Twisted block solve (pdipm_srbd.hpp FastCtx::solve), w / v in registers.
@@ -854,8 +895,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       }
     }
 #pragma unroll
-    for (int t = 0; t < Lo::SE; ++t)
-      if (lane + TPB * t < p) bw[lane + TPB * t] = former_b(lane + TPB * t, N, F);
+    for (int t = 0; t < Lo::SE; ++t) {
+      const auto q = RegCtx<N>::erow(lane, t);
+      if (q.valid) bw[q.e] = former_b(q.e, N, F);
+    }
 #pragma unroll
     for (int t = 0; t < SI; ++t)
       if (lane + TPB * t < m) dw[lane + TPB * t] = former_d(lane + TPB * t, N, P[2], P[12], mu);
@@ -1064,7 +1107,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         if (ul + TPB * t < m) b += C.rs[t] * C.rs[t];
 #pragma unroll
       for (int t = 0; t < Lo::SE; ++t)
-        if (ul + TPB * t < p) c += C.re[t] * C.re[t];
+        if (RegCtx<N>::erow(ul, t).valid) c += C.re[t] * C.re[t];
       res0 = sqrt(C.block_sum(a));
       res1 = sqrt(C.block_sum(b));
       res2 = sqrt(C.block_sum(c));
