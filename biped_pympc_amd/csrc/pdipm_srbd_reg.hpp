@@ -197,12 +197,17 @@ __device__ __forceinline__ double ncol(const double* nd, int col, const double* 
   return (a0 + a1) + a2;
 }
 
-// (G xu)_k over the 4 columns of row k's foot
+// Structural nonzeros of a foot's 8 inequality rows k over its columns (fx, fy, fz, my)
+// (srbd_constraints.py:193-222): every row has fz; rows 0,1 also fx, rows 2,3 fy, rows 4,5 my,
+// rows 6,7 nothing else. g_other(k) is that other column's position (0 for rows 6,7, where G is a
+// stored structural zero, so the formula stays uniform across lanes).
+__host__ __device__ constexpr int g_other(int k) { return k < 2 ? 0 : (k < 4 ? 1 : (k < 6 ? 3 : 0)); }
+
+// (G xu)_k over row k's structural nonzeros (fz and the other column)
 __device__ __forceinline__ double grow4(const double* gf, int k, const double* xu) {
-  const int f = k >> 3;
+  const int f = k >> 3, o = g_other(k & 7);
   const double* g = gf + 4 * k;
-  return (g[0] * xu[foot_colj(f, 0)] + g[1] * xu[foot_colj(f, 1)]) +
-         (g[2] * xu[foot_colj(f, 2)] + g[3] * xu[foot_colj(f, 3)]);
+  return g[o] * xu[foot_colj(f, o)] + g[2] * xu[foot_colj(f, 2)];
 }
 
 template <int N>
@@ -420,16 +425,18 @@ struct RegCtx {
 #pragma unroll
         for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? Hu[foot_colj(f, r)] + kBeta : 0.0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < 8; ++k) {  // + G_k^T lam_k G_k over row k's structural nonzeros
         const double lam = VV[16 * i + 8 * f + k];
         const double* g4 = Gf + 4 * (8 * f + k);
-        double gl[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) gl[b] = g4[b];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * gl[r] * gl[c];
+        const double gz = g4[2];
+        a[5] += lam * gz * gz;  // (fz, fz)
+        if (k < 6) {
+          const int o = g_other(k);  // fx, fy or my (k is unrolled: constant)
+          const double go = g4[o];
+          a[o * (o + 1) / 2 + o] += lam * go * go;
+          if (o < 2) a[3 + o] += lam * gz * go;  // (fz, o)
+          else a[8] += lam * go * gz;            // (my, fz)
+        }
       }
       sweep_inverse<4, true>(a);
 #pragma unroll
@@ -652,17 +659,23 @@ struct RegCtx {
         const int i = lane >> 1, f = lane & 1, b = 12 * i;
         const double* vv = VV + 16 * i + 8 * f;
         double rv[4];
+        const double* g = Gf + 32 * f;  // (G^T vv)_a over column a's structural rows
+        double vk[8];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const double* g = Gf + 32 * f + a;
-          double g0 = 0.0, g1 = 0.0;
+        for (int k = 0; k < 8; ++k) vk[k] = vv[k];
+        const double gfx = g[0] * vk[0] + g[4] * vk[1];
+        const double gfy = g[9] * vk[2] + g[13] * vk[3];
+        const double gmy = g[19] * vk[4] + g[23] * vk[5];
+        double gz0 = 0.0, gz1 = 0.0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            g0 += g[4 * k] * vv[k];
-            g1 += g[4 * (k + 4)] * vv[k + 4];
-          }
-          rv[a] = -RXu[b + foot_colj(f, a)] - (g0 + g1);
+        for (int k = 0; k < 4; ++k) {
+          gz0 += g[4 * k + 2] * vk[k];
+          gz1 += g[4 * (k + 4) + 2] * vk[k + 4];
         }
+        rv[0] = -RXu[b + foot_colj(f, 0)] - gfx;
+        rv[1] = -RXu[b + foot_colj(f, 1)] - gfy;
+        rv[2] = -RXu[b + foot_colj(f, 2)] - (gz0 + gz1);
+        rv[3] = -RXu[b + foot_colj(f, 3)] - gmy;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
