@@ -37,7 +37,8 @@ struct RegLayout {
   static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 144, K0 = Gf + 64, K1 = K0 + 78,
                        Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, TRI = SG + 16,
                        DV = TRI + 10,
-                       X = DV + 78 * N, Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
+                       X = DV + 80 * N,  // stage blocks of 80 doubles (78 used, kDvSlot)
+                       Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
                        RED = DYm + 2 * N,  // block reductions of a 2-wave QP: 2 slot pairs
                        total = RED + (TPB > 64 ? 4 : 0);
@@ -59,7 +60,23 @@ template <int N>
 __host__ __device__ constexpr int dv_pos(int i) {
   return i < N / 2 ? 2 * i : (i == N / 2 ? N - 1 : 2 * (N - 1 - i) + 1);
 }
-constexpr int kDvBytes = 78 * 8;  // one packed-lower 12x12 block
+// One symmetric 12x12 stage block: 78 distinct elements in 80 double slots. The slot of element
+// (r, c) = (c, r) is kDvSlot[packed index r(r+1)/2 + c] (scripts/dv_slots.py): in every column the
+// 12 rows sit in distinct slots mod 16, and the two twisted groups' blocks of a step are 80 doubles
+// (= 16 mod 32) apart, so the 24 lanes of a chain load or store hit 24 distinct LDS bank pairs
+// (the packed layout with stride 78 averaged 2.4 bank cycles per access). Every access to a block
+// goes through this map: the per-lane offset tables below and the S_ii build's entry slots.
+constexpr int kDvStride = 80;
+constexpr int kDvBytes = kDvStride * 8;
+constexpr uint8_t kDvSlot[78] = {77, 58, 32, 73, 46, 5,  52, 54, 50, 65, 53, 75, 31, 14, 76, 30, 69, 71, 64, 20,
+                                 15, 48, 8,  3,  9,  23, 28, 21, 6,  49, 43, 44, 29, 18, 78, 51, 19, 61, 42, 79,
+                                 41, 24, 33, 39, 70, 55, 2,  22, 37, 40, 67, 27, 26, 68, 60, 66, 57, 36, 59, 1,
+                                 45, 74, 56, 0,  63, 7,  11, 12, 72, 10, 35, 25, 4,  16, 34, 62, 38, 13};
+static __constant__ uint8_t c_dvslot[78] = {77, 58, 32, 73, 46, 5,  52, 54, 50, 65, 53, 75, 31, 14, 76, 30,
+                                            69, 71, 64, 20, 15, 48, 8,  3,  9,  23, 28, 21, 6,  49, 43, 44,
+                                            29, 18, 78, 51, 19, 61, 42, 79, 41, 24, 33, 39, 70, 55, 2,  22,
+                                            37, 40, 67, 27, 26, 68, 60, 66, 57, 36, 59, 1,  45, 74, 56, 0,
+                                            63, 7,  11, 12, 72, 10, 35, 25, 4,  16, 34, 62, 38, 13};
 
 // Byte offset, inside a step's block pair, of element (row r, column c) of chain lane l (group
 // g = l >> 4, row r = min(l & 15, 11), both in the group's coordinates): packed-lower slot of
@@ -73,7 +90,8 @@ constexpr ChainOffs make_chain_offs() {
   for (int l = 0; l < 32; ++l) {
     const int g = l >> 4, r = (l & 15) < 12 ? (l & 15) : 11;
     const int pr = g ? perm12c(r) : r;
-    for (int c = 0; c < 12; ++c) t.o[l][c] = (uint32_t)(8 * sym_idx_c(pr, g ? perm12c(c) : c) + kDvBytes * g);
+    for (int c = 0; c < 12; ++c)
+      t.o[l][c] = (uint32_t)(8 * kDvSlot[sym_idx_c(pr, g ? perm12c(c) : c)] + kDvBytes * g);
   }
   return t;
 }
@@ -457,7 +475,7 @@ struct RegCtx {
     const int lw = lane & 63, wv = lane >> 6;
     if (lw < 63) {  // dense x dense: lw = 21 q' + k -> entry k of stages NQ t + q, q = 3 wv + q'
       const int q = 3 * wv + lw / 21, k = lw - 21 * (lw / 21);
-      const int rc = TRI[k], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
+      const int rc = TRI[k], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c, sl = c_dvslot[sy];
       double vr[2][4], vc[2][4];
 #pragma unroll
       for (int f = 0; f < 2; ++f)
@@ -483,14 +501,14 @@ struct RegCtx {
               v += vr[f][a] * tt;
             }
           }
-          DV[78 * dv_pos<N>(i) + sy] = v;
+          DV[kDvStride * dv_pos<N>(i) + sl] = v;
         }
       }
     }
     if (lw < 57) {  // the 57 entries with a sparse index (rows {3,4,5,9,10,11} of N hold one entry
                       // per foot, at position r % 3), one stage per trip; for a sparse x sparse entry
                       // the 4-term sum over the "dense" index meets N's zeros, so it is exact too
-      const int rc = TRI[21 + lw], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c;
+      const int rc = TRI[21 + lw], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c, sl = c_dvslot[sy];
       const bool rs = (r % 6) >= 3;
       const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
       double nd[2][4], ns[2];
@@ -515,7 +533,7 @@ struct RegCtx {
           for (int b = 0; b < 4; ++b) tt += ph_[po[b]] * nd[f][b];
           v += ns[f] * tt;
         }
-        DV[78 * dv_pos<N>(i) + sy] = v;
+        DV[kDvStride * dv_pos<N>(i) + sl] = v;
       }
     }
     __syncthreads();
