@@ -90,6 +90,21 @@ def load_pmc(N: int, B: int, K: int):
     return None, None
 
 
+def load_sq(N: int, B: int, K: int):
+    """VALU / LDS busy shares of the bench kernel from the committed rocprofv3 SQ-counter summary
+    (scripts/gpu_sq_counters.sh + scripts/sq_summary.py --json)."""
+    name = solver_kernel_name(N)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_counters_*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if (d.get("horizon") == N and d.get("batch") == B and d.get("iters") == K
+                and name in (d.get("kernel") or "") and d.get("utilisation")):
+            return dict(d["utilisation"], source=os.path.relpath(path, ROOT))
+    return None
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +204,7 @@ def main():
                      "(SURVEY 8d) x iterations x QPs per launch. Bytes = former inputs in + "
                      "solution out per QP (fused step)." if fused else
                      "FP64 compute roof; flops as SURVEY 8d; bytes = QP in + solution out."),
+            "utilisation": load_sq(N, B, K),  # measured VALU / LDS busy shares (what bounds it)
             "hbm": {"achieved_GBs": round(hbm_bytes / (ms_main * 1e-3) / 1e9, 2),
                     "peak_GBs": PEAK_HBM_GBS,
                     "frac": round(hbm_bytes / (ms_main * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),

@@ -17,6 +17,11 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("dirs", nargs="+")
     p.add_argument("--kernel", default="mpc_step_reg_kernel<10>")
+    p.add_argument("--json", help="also write the per-wave averages + derived utilisation here")
+    p.add_argument("--waves-per-simd", type=int, default=2)
+    p.add_argument("--horizon", type=int, default=10)
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--iters", type=int, default=10)
     a = p.parse_args()
     acc, grid = defaultdict(list), {}
     for d in a.dirs:
@@ -29,10 +34,25 @@ def main():
     if not acc:
         raise SystemExit(f"no dispatches of {a.kernel}")
     print(f"kernel {a.kernel}: per-wave averages (one QP per wave)")
+    per_wave = {}
     for k in sorted(acc):
         waves = grid[k] // 64
         v = sum(acc[k]) / len(acc[k])
+        per_wave[k] = v / waves
         print(f"  {k:24s} {v / waves:12.1f}   (dispatches {len(acc[k])}, waves {waves})")
+    if a.json:
+        import json
+        wc = per_wave.get("SQ_WAVE_CYCLES")
+        w = a.waves_per_simd
+        util = None
+        if wc:
+            # a SIMD runs w waves at a time: VALU-active share of the SIMD; LDS-active share of the
+            # CU's LDS pipe (4 SIMDs x w waves issue into one LDS)
+            util = {"valu_busy": round(w * per_wave.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3),
+                    "lds_busy": round(4 * w * per_wave.get("SQ_ACTIVE_INST_LDS", 0) / wc, 3),
+                    "waves_per_simd": w}
+        json.dump({"kernel": a.kernel, "horizon": a.horizon, "batch": a.batch, "iters": a.iters,
+                   "per_wave": per_wave, "utilisation": util}, open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
