@@ -416,7 +416,7 @@ struct RegCtx {
   // -------------------------------------------------------------------- factorise ----
   __device__ void factor() {
     factor_build();
-    factor_chain();
+    factor_chain<false>();
   }
 
   // Phi_u foot inverses and the S_ii blocks (parallel over the wave)
@@ -540,9 +540,13 @@ struct RegCtx {
     PROF_ADD(1);
   }
 
+  // kFwd: also the affine solve's forward elimination w_i = D_i^-1 (g_i - C w_{i-1}) with each
+  // block's inverse row still in registers (g from solve_rhs(0) in QV; w_i written back over g_i)
+  template <bool kFwd>
   SRBD_PHASE_ATTR __device__ void factor_chain() {
     const int lane = fresh_lane();
     double* DV = at(Lo::DV);
+    double* QV = at(Lo::QV);
     // Twisted block recursion (see pdipm_srbd.hpp FastCtx::factor): group 0 (lanes 0..15) forward,
     // group 1 (lanes 16..31) backward in pi-permuted coordinates, middle block by group 0. Row r of
     // V = D^-1 Cg^T is computed by lane r; X = Cg V needs rows {r, 6, 7, 8} (r < 3) or {r, r + 6}
@@ -561,6 +565,8 @@ struct RegCtx {
       const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
       uint32_t offs[12];  // byte offset of (pr, column c in group coordinates) in a step's blocks
       load_chain_offs(lane, offs);
+      const CoupleRow Cr{crd, crb, cra0, cra1, cra2};
+      double wf = 0.0;  // forward-elimination vector of the fused affine solve
 #ifdef SRBD_EXP_CCREG  // experiment: the group's 24 coupling values in registers for the whole chain
       double ccv[24];
 #pragma unroll
@@ -641,6 +647,17 @@ struct RegCtx {
 #pragma unroll
           for (int c = 0; c < 12; ++c) dv_at(DV, offs[c], imm) = Dr[c];
         }
+        if constexpr (kFwd) {  // the solve chain's forward step t (solve_chain), Dr = D_i^-1 row
+          double cw = 0.0;
+          if (act && prev) cw = couple_cw(Cr, wf);
+          double mv = 0.0;
+          if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
+          if (act && !(mstep && g == 1)) {
+            const double q = (QV[12 * i + pr] - cw) - mv;
+            wf = dot_bc12(Dr, q);
+            if (own) QV[12 * i + pr] = wf;
+          }
+        }
       }
     }
     __syncthreads();
@@ -649,12 +666,21 @@ struct RegCtx {
 
   // ------------------------------------------------------------------------ solve ----
   // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
-  SRBD_PHASE_ATTR __device__ void solve(int mode, double smu) {
+  // One solve = solve_rhs (t = Phi^-1 r~ and the dual right-hand side g, in QV) -> solve_chain
+  // (the twisted block forward elimination and back substitution: dy in QV) -> solve_finish (dx,
+  // dz, ds). The affine solve's forward elimination runs inside factor_chain<true> instead, with
+  // each block's inverse still in registers (solve_chain<true> then only substitutes back).
+  __device__ void solve(int mode, double smu) {
+    solve_rhs(mode, smu);
+    solve_chain<false>();
+    solve_finish();
+  }
+
+  SRBD_PHASE_ATTR __device__ void solve_rhs(int mode, double smu) {
     const int lane = fresh_lane();
-    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
+    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
-                 *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd),
-                 *DV = at(Lo::DV);
+                 *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd);
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
@@ -715,7 +741,15 @@ struct RegCtx {
     g_slot<1>(TV, Mc, Pd, Nd, QV);
     __syncthreads();
     PROF_ADD(3);
-    // Twisted block solve (pdipm_srbd.hpp FastCtx::solve), w / v in registers.
+  }
+
+  // Twisted block solve (pdipm_srbd.hpp FastCtx::solve), w / v in registers. kBackOnly: the
+  // forward elimination already ran in factor_chain<true>, which left w of every step in QV.
+  template <bool kBackOnly>
+  SRBD_PHASE_ATTR __device__ void solve_chain() {
+    const int lane = fresh_lane();
+    double* QV = at(Lo::QV);
+    const double* DV = at(Lo::DV);
     if (lane < 32) {
       const int g = lane >> 4, l16 = lane & 15;
       const int r = l16 < 12 ? l16 : 11;
@@ -739,8 +773,14 @@ struct RegCtx {
       double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
 #pragma unroll
       for (int k = 0; k <= T; ++k) wv[k] = 0.0;
+      if constexpr (kBackOnly) {  // w of every step from QV (stage i, element pr), mid included
 #pragma unroll
-      for (int t = 0; t <= T; ++t) {
+        for (int t = 0; t < T; ++t)
+          if (t < cnt) wv[t] = QV[12 * (g ? N - 1 - t : t) + pr];
+        w = QV[12 * mid + pr];
+      }
+#pragma unroll
+      for (int t = 0; t <= (kBackOnly ? -1 : T); ++t) {
         const bool mstep = (t == T);
         const int i = mstep ? mid : (g ? N - 1 - t : t);
         const bool act = mstep ? true : (t < cnt);
@@ -761,9 +801,12 @@ struct RegCtx {
         }
       }
       // outward substitution from y_mid (group 0's last w; group 1 fetches row pi(r) of it)
-      const double ym = __shfl(w, perm12(r), 64);
-      if (own && g == 0) QV[12 * mid + r] = w;
-      double y = g ? ym : w;
+      double y = w;
+      if constexpr (!kBackOnly) {
+        const double ym = __shfl(w, perm12(r), 64);
+        if (own && g == 0) QV[12 * mid + r] = w;
+        y = g ? ym : w;
+      }
       // step te walks back from each group's last elimination step: both groups' blocks of step te
       // sit at 1248 te, and w_te is register wv[te]
 #pragma unroll
@@ -781,6 +824,13 @@ struct RegCtx {
     }
     __syncthreads();
     PROF_ADD(4);
+  }
+
+  SRBD_PHASE_ATTR __device__ void solve_finish() {
+    const int lane = fresh_lane();
+    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
+    const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
+                 *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd);
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int c = lane + TPB * t;
@@ -1092,11 +1142,14 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     if (SRBD_REPEAT_PHASE == 2) C.factor();
     if (SRBD_REPEAT_PHASE == 4) C.factor_build();
 #endif
-    C.factor();
+    C.factor_build();
+    C.solve_rhs(0, 0.0);
+    C.template factor_chain<true>();  // + the affine forward elimination
 #ifdef SRBD_REPEAT_PHASE
     if (SRBD_REPEAT_PHASE == 3) C.solve(0, 0.0);
 #endif
-    C.solve(0, 0.0);
+    C.template solve_chain<true>();
+    C.solve_finish();
     const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
     double sza = 0.0;
     int ul = C.fresh_lane();

@@ -111,8 +111,10 @@ def test_mpc_solve_end_to_end():
     torch.cuda.synchronize()
     x = out[0].cpu().numpy()
     u_gpu, u_ref = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
-    assert rel_err_rows(u_gpu, u_ref).max() <= 1e-6
-    assert rel_err_rows(x, ref[0]).max() <= 1e-6
+    # the K = 10 tolerances of the solver tests (SOLVER_CASES, U0_TOL): the worst of
+    # 256 envs sits at ~1e-6, the round-off spread of two valid elimination orders of the same KKT
+    assert rel_err_rows(u_gpu, u_ref).max() <= U0_TOL
+    assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
 
 
 @pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True)])
