@@ -144,6 +144,36 @@ __device__ __forceinline__ void fmac_rows678_4(double& x0, double& x1, double& x
 // lane i of every 16-lane row <- lane i - 6 (rows 9..11 fetch rows 3..5)
 __device__ __forceinline__ double shr6(double v) { return __builtin_amdgcn_mov_dpp(v, 0x116, 0xF, 0xF, true); }
 
+// V = D^-1 C^T row by row: V[c] = Dr[c] C[c][c] + (c < 3: sum_k Dr[6 + k] C[c][6 + k])
+// + (3 <= c < 6: Dr[c + 6] C[c][c + 6]), the coefficients of row c broadcast from lane c, which
+// holds C's row c as (d, a0, a1, a2, b)
+#define SRBD_VROW_A(C)                                                                              \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C)               \
+      SRBD_FMAC_BC("%0", "%6", "%7", C) SRBD_FMAC_BC("%0", "%8", "%9", C) "s_nop 1\n"              \
+      : "=&v"(V[C])                                                                                 \
+      : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(a0), "v"(Dr[6]), "v"(a1), "v"(Dr[7]), "v"(a2), "v"(Dr[8]))
+#define SRBD_VROW_B(C)                                                                              \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C) "s_nop 1\n"  \
+      : "=&v"(V[C])                                                                                 \
+      : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(b), "v"(Dr[C + 6]))
+#define SRBD_VROW_D(C)                                                                              \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) "s_nop 1\n" : "=&v"(V[C]) : "0"(0.0), "v"(d), "v"(Dr[C]))
+__device__ __forceinline__ void v_rows(double (&V)[12], const double (&Dr)[12], double d, double a0, double a1,
+                                       double a2, double b) {
+  SRBD_VROW_A(0);
+  SRBD_VROW_A(1);
+  SRBD_VROW_A(2);
+  SRBD_VROW_B(3);
+  SRBD_VROW_B(4);
+  SRBD_VROW_B(5);
+  SRBD_VROW_D(6);
+  SRBD_VROW_D(7);
+  SRBD_VROW_D(8);
+  SRBD_VROW_D(9);
+  SRBD_VROW_D(10);
+  SRBD_VROW_D(11);
+}
+
 // (C w)_r and (C^T y)_r of the compact stage coupling for one vector held one element per lane:
 // C has the diagonal, rows 0..2 x columns 6..8 and (r, r + 6) for 3 <= r < 6, so each is a local
 // product, one row shift and three broadcast-FMAs (instead of a dense 12-term broadcast dot).
@@ -567,13 +597,6 @@ struct RegCtx {
       load_chain_offs(lane, offs);
       const CoupleRow Cr{crd, crb, cra0, cra1, cra2};
       double wf = 0.0;  // forward-elimination vector of the fused affine solve
-#ifdef SRBD_EXP_CCREG  // experiment: the group's 24 coupling values in registers for the whole chain
-      double ccv[24];
-#pragma unroll
-      for (int k = 0; k < 24; ++k) ccv[k] = cc[k];
-#else
-      const double* ccv = cc;
-#endif
       double Dr[12];
 #pragma unroll
       for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
@@ -598,13 +621,9 @@ struct RegCtx {
           if (prev) {
 #endif
             double V[12];
-#pragma unroll
-            for (int c = 0; c < 12; ++c) {
-              double v = Dr[c] * ccv[c];
-              if (c < 3) v += (Dr[6] * ccv[12 + 3 * c] + Dr[7] * ccv[13 + 3 * c]) + Dr[8] * ccv[14 + 3 * c];
-              else if (c < 6) v += Dr[c + 6] * ccv[21 + c - 3];
-              V[c] = v;
-            }
+            // V[c] = sum_k Dr[k] C[c][k]: row c of C is lane c's own coupling row (crd, cra*, crb),
+            // broadcast inside the FMAs (row_newbcast:c) instead of re-read from LDS every step
+            v_rows(V, Dr, crd, cra0, cra1, cra2, crb);
             if (!mstep) {  // S - X accumulated in place
 #pragma unroll
               for (int c = 0; c < 12; ++c) Sr[c] = (Sr[c] - crd * V[c]) - crb * shl6(V[c]);
