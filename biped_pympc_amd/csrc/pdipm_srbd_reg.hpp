@@ -506,14 +506,23 @@ struct RegCtx {
     if (lw < 63) {  // dense x dense: lw = 21 q' + k -> entry k of stages NQ t + q, q = 3 wv + q'
       const int q = 3 * wv + lw / 21, k = lw - 21 * (lw / 21);
       const int rc = TRI[k], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c, sl = c_dvslot[sy];
-      double vr[2][4], vc[2][4];
+      // n_r Phi^-1 n_c^T = sum over packed (a >= b) of Phi^-1_ab w_ab with the stage-invariant pair
+      // products w_aa = n_ra n_ca, w_ab = n_ra n_cb + n_rb n_ca: 10 FMAs per foot and stage, not 20
+      double w[2][10];
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
+      for (int f = 0; f < 2; ++f) {
+        double vr[4], vc[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          vr[f][a] = Nd[r * 12 + foot_colj(f, a)];
-          vc[f][a] = Nd[c * 12 + foot_colj(f, a)];
+          vr[a] = Nd[r * 12 + foot_colj(f, a)];
+          vc[a] = Nd[c * 12 + foot_colj(f, a)];
         }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b <= a; ++b)
+            w[f][a * (a + 1) / 2 + b] = a == b ? vr[a] * vc[a] : vr[a] * vc[b] + vr[b] * vc[a];
+      }
       const double k0 = K0[sy], k1 = K1[sy];
 #pragma unroll
       for (int t = 0; t < (N + NQ - 1) / NQ; ++t) {
@@ -524,12 +533,7 @@ struct RegCtx {
           for (int f = 0; f < 2; ++f) {
             const double* ph_ = PHs + 20 * i + 10 * f;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) {
-              double tt = 0.0;
-#pragma unroll
-              for (int b = 0; b < 4; ++b) tt += ph_[sym_idx(a, b)] * vc[f][b];
-              v += vr[f][a] * tt;
-            }
+            for (int e = 0; e < 10; ++e) v += ph_[e] * w[f][e];
           }
           DV[kDvStride * dv_pos<N>(i) + sl] = v;
         }
@@ -541,13 +545,13 @@ struct RegCtx {
       const int rc = TRI[21 + lw], r = rc & 15, c = rc >> 4, sy = r * (r + 1) / 2 + c, sl = c_dvslot[sy];
       const bool rs = (r % 6) >= 3;
       const int sp = rs ? r : c, dn = rs ? c : r, as = sp % 3;
-      double nd[2][4], ns[2];
+      double wn[2][4];  // stage-invariant products n_sp,as * n_dn,b: 4 FMAs per foot and stage
       int po[4];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
+        const double ns = Nd[sp * 12 + foot_colj(f, as)];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) nd[f][b] = Nd[dn * 12 + foot_colj(f, b)];
-        ns[f] = Nd[sp * 12 + foot_colj(f, as)];
+        for (int b = 0; b < 4; ++b) wn[f][b] = ns * Nd[dn * 12 + foot_colj(f, b)];
       }
 #pragma unroll
       for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
@@ -558,10 +562,8 @@ struct RegCtx {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const double* ph_ = PHs + 20 * i + 10 * f;
-          double tt = 0.0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) tt += ph_[po[b]] * nd[f][b];
-          v += ns[f] * tt;
+          for (int b = 0; b < 4; ++b) v += ph_[po[b]] * wn[f][b];
         }
         DV[kDvStride * dv_pos<N>(i) + sl] = v;
       }
