@@ -46,8 +46,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch-per-gpu", type=int, default=4096)
     p.add_argument("--horizon", type=int, default=10)
     p.add_argument("--iters", type=int, default=10)
