@@ -24,6 +24,9 @@ def _check_batch(tensors, widths, B: int, what: str):
             continue
         if not t.is_cuda or t.dtype != torch.float64:
             raise TypeError(f"{what}: input {i} must be a CUDA float64 tensor")
+        if t.device.index != torch.cuda.current_device():  # launches go to the current device's stream
+            raise ValueError(f"{what}: input {i} is on {t.device}, the current device is "
+                             f"cuda:{torch.cuda.current_device()}")
         if t.numel() != B * w:
             raise ValueError(f"{what}: input {i} has {t.numel()} elements, expected {B}x{w}")
         if not t.is_contiguous():
@@ -38,6 +41,7 @@ def qp_former(inputs: list[torch.Tensor], N: int, outputs: list[torch.Tensor] | 
     if outputs is None:
         outputs = [torch.empty((B, w), dtype=torch.float64, device=inputs[0].device)
                    for w in d.former_out_nnz]
+    _check_batch(outputs, d.former_out_nnz, B, "qp_former outputs")
     L = _native.lib()
     rc = L.srbd_qp_former(N, B, _native.ptr_array([t.data_ptr() for t in inputs]),
                           _native.ptr_array([t.data_ptr() for t in outputs]), _stream_ptr())
@@ -63,6 +67,7 @@ def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_
     _check_batch(ins, d.solver_in_nnz, B, "pdipm")
     if outputs is None:
         outputs = _alloc_solver_outputs(B, N, qp[0].device)
+    _check_batch(outputs, d.solver_out_nnz, B, "pdipm outputs")
     L = _native.lib()
     ptrs = _native.ptr_array([t.data_ptr() if t is not None else 0 for t in ins])
     outp = _native.ptr_array([t.data_ptr() for t in outputs])
@@ -113,6 +118,9 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     _check_batch(former_inputs, d.former_in_nnz, B, "mpc_solve")
     if buffers is None or buffers.B != B or buffers.N != N:
         buffers = MPCSolveBuffers.allocate(N, B, former_inputs[0].device)
+    _check_batch(buffers.outputs, d.solver_out_nnz, B, "mpc_solve outputs")
+    if buffers.workspace.device != former_inputs[0].device:
+        raise ValueError(f"mpc_solve: workspace on {buffers.workspace.device}, inputs on {former_inputs[0].device}")
     L = _native.lib()
     rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
                           _native.ptr_array([t.data_ptr() for t in former_inputs]),

@@ -215,3 +215,26 @@ def test_cusadi_dropin_random_inputs(fn_kind):
     dense = cf.getDenseOutput(2 if fn_kind == "qp_former" else 0).cpu().numpy()
     if fn_kind == "qp_former":
         assert np.allclose(dense, layout.to_dense(ref[2], *layout.ccs_A(N), (14 * N, 24 * N)), atol=1e-12)
+
+
+def test_api_rejects_bad_buffers():
+    """Wrong widths, dtypes or host tensors are refused before any launch (the C-ABI trusts sizes)."""
+    N, B = 10, 8
+    wl = make_workload(B, N, seed=2)
+    ins = _cuda(wl.inputs)
+    d = layout.Dims(N)
+    bad_out = [torch.empty((B, w + 1), dtype=torch.float64, device="cuda") for w in d.former_out_nnz]
+    with pytest.raises(ValueError):
+        solver.qp_former(ins, N, outputs=bad_out)
+    with pytest.raises(TypeError):
+        solver.qp_former([t.cpu() for t in ins], N)
+    with pytest.raises(TypeError):
+        solver.qp_former([t.float() for t in ins], N)
+    H, f, A, b, G, dd = solver.qp_former(ins, N)
+    qp = [H, G, A, f, dd, b]
+    with pytest.raises(ValueError):
+        solver.pdipm(qp, None, N, 1, outputs=[torch.empty((B, 3), dtype=torch.float64, device="cuda")] * 6)
+    bufs = solver.MPCSolveBuffers.allocate(N, B, "cuda")
+    bufs.outputs[0] = torch.empty((B, 5), dtype=torch.float64, device="cuda")
+    with pytest.raises(ValueError):
+        solver.mpc_solve(ins, N, 1, buffers=bufs)
