@@ -196,6 +196,7 @@ int srbd_qp_former(int horizon, int batch, const double* const* inputs, double* 
                    void* stream) {
   if (!horizon_ok(horizon) || batch < 0 || !inputs || !outputs)
     return set_error(kErrInvalid, "srbd_qp_former: bad arguments");
+  if (batch == 0) return 0;  // empty batch: buffers may be null (zero-size allocations)
   srbd::FormerArgs a{};
   for (int i = 0; i < 17; ++i) {
     if (!inputs[i]) return set_error(kErrInvalid, "srbd_qp_former: null input");
@@ -214,6 +215,7 @@ static int pdipm_common(int horizon, int n_iter, int batch, double y0, int init_
                         const double* const* inputs, double* const* outputs, void* stream) {
   if (!horizon_ok(horizon) || n_iter < 1 || batch < 0 || !inputs || !outputs)
     return set_error(kErrInvalid, "srbd_pdipm: bad arguments");
+  if (batch == 0) return 0;
   srbd::SolverArgs a{};
   const int nin = init_mode ? 6 : 10;
   for (int i = 0; i < nin; ++i) {

@@ -238,3 +238,34 @@ def test_api_rejects_bad_buffers():
     bufs.outputs[0] = torch.empty((B, 5), dtype=torch.float64, device="cuda")
     with pytest.raises(ValueError):
         solver.mpc_solve(ins, N, 1, buffers=bufs)
+
+
+@pytest.mark.parametrize("N", [10, 20])
+@pytest.mark.parametrize("B", [1, 3, 13, 509])
+def test_ragged_batches(N, B):
+    """Batch sizes that fill neither a former workgroup (4 envs) nor the 8 XCDs evenly: the
+    XCD-contiguous env map (srbd_common.hpp xcd_item) and the grid tails must cover every env once."""
+    K = 10
+    wl = make_workload(B, N, seed=4000 + B, random_gait=True, residuals=True)
+    ins = _cuda(wl.inputs)
+    ref = oracle.mpc_solve(N, K, wl.inputs, y0=1.0)
+    fused = [t.clone() for t in solver.mpc_solve(ins, N, K, y0=1.0, fused=True)]
+    plain = solver.mpc_solve(ins, N, K, y0=1.0, fused=False)
+    torch.cuda.synchronize()
+    for a, c in zip(fused, plain):
+        assert torch.equal(a, c)
+    x = fused[0].cpu().numpy()
+    assert np.all(np.isfinite(x))
+    u_gpu, u_ref = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
+    assert rel_err_rows(u_gpu, u_ref).max() <= U0_TOL
+    assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
+
+
+def test_empty_batch_is_a_no_op():
+    N = 10
+    wl = make_workload(1, N, seed=1)
+    empty = [torch.from_numpy(np.ascontiguousarray(a[:0])).cuda() for a in wl.inputs]
+    out = solver.mpc_solve(empty, N, 10)
+    former = solver.qp_former(empty, N)
+    torch.cuda.synchronize()
+    assert all(t.shape[0] == 0 for t in out) and all(t.shape[0] == 0 for t in former)

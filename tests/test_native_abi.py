@@ -79,3 +79,7 @@ def test_bad_arguments_return_errors_without_touching_the_gpu():
     assert L.srbd_pdipm(10, 5, 4, nulls, nulls, None) != 0  # null pointers
     assert "null input" in _native.last_error()
     assert L.srbd_evaluate_pdipm(40, 5, None, None, None, 4) < 0
+    # an empty batch is a successful no-op, whatever the (zero-size) buffers point to
+    assert L.srbd_qp_former(10, 0, nulls, nulls, None) == 0
+    assert L.srbd_pdipm(10, 5, 0, nulls, nulls, None) == 0
+    assert L.srbd_pdipm_cold(10, 5, 0, 1.0, nulls, nulls, None) == 0
