@@ -1,6 +1,6 @@
 """Diagnostic: marginal cost of each solver phase in the real (2 waves/SIMD) context.
 
-Builds variants of libsrbd_mpc.so with -DSRBD_REPEAT_PHASE=k (k = 1 residuals, 2 factorisation,
+Builds variants of libsrbd_mpc.so with -DSRBD_REPEAT_PHASE=k (k = 1 residuals, 2 factorisation, 4 its S_ii build,
 3 affine solve: each idempotent, run twice per Newton iteration) into /tmp and times the N=10
 solver launch with each; the difference to the base build is that phase's cost per launch.
 Run on the GPU box: python scripts/phase_ablation.py [N] [B] [K]
@@ -13,7 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 10
-names = {0: "base", 1: "residuals", 2: "factorisation (parallel + chain)", 3: "one solve (parallel + chains)"}
+names = {0: "base", 1: "residuals", 2: "factorisation (parallel + chain)", 4: "factorisation: S_ii build only",
+         3: "one solve (parallel + chains)"}
 res = {}
 for k in names:
     lib = f"/tmp/libsrbd_mpc_rep{k}.so"
