@@ -19,6 +19,9 @@
 #include "pdipm_srbd.hpp"
 #include "qp_former.hpp"
 
+#ifndef SRBD_PROGRESS_PRIO
+#define SRBD_PROGRESS_PRIO 1  // progress-ordered wave priority (A/B switch for scripts/variant_bench.py)
+#endif
 #ifndef SRBD_PHASE_ATTR
 #define SRBD_PHASE_ATTR  // diagnostic builds: __attribute__((noinline)) to read one phase ISA alone
 #endif
@@ -945,6 +948,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= (kFused ? fa.batch : args.batch)) return;
+#ifdef SRBD_HWID_DUMP  // diagnostic builds only: residual slots get HW_ID, XCC_ID, start / end time
+  const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int lane = threadIdx.x;
   constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
   RegCtx<N> C;
@@ -1153,6 +1159,17 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   PROF_MARK_CTX(C);
   const int n_iter = kFused ? fa.n_iter : args.n_iter;
   for (int it = 0; it < n_iter; ++it) {
+    if constexpr (TPB == 64 && SRBD_PROGRESS_PRIO) {
+      // Wave priority falls with this QP's progress (3 over the first quarter of the iterations, 0
+      // over the last): of the two waves sharing a SIMD the one further behind issues first, so
+      // they finish together instead of the younger wave running its tail alone (the SIMD's
+      // default is oldest-first). Not at N = 20, whose QPs span two waves joined by barriers.
+      const int lvl = 3 - (4 * it) / n_iter;
+      if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
 #ifdef SRBD_REPEAT_PHASE  // diagnostic builds only (scripts/phase_ablation.py): run one idempotent
                           // phase twice so the timing difference is its marginal cost
     if (SRBD_REPEAT_PHASE == 1) (void)C.residuals();
@@ -1244,6 +1261,12 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     ro[2] = res2;
     ro[3] = mu_new;
     mo[0] = mu_new;
+#ifdef SRBD_HWID_DUMP
+    ro[0] = (double)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    ro[1] = (double)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+    ro[2] = (double)dbg_t0;
+    ro[3] = (double)__builtin_amdgcn_s_memrealtime();
+#endif
   }
 }
 

@@ -1,6 +1,6 @@
 """Fused-step A/B of compile-time variants on one GPU box (the bench's own kernel and timing).
 
-python scripts/variant_bench.py [--horizon N] [--rounds R] NAME=FLAGS [NAME=FLAGS ...]
+python scripts/variant_bench.py [--horizon N] [--rounds R] [--batch B] NAME=FLAGS [NAME=FLAGS ...]
 Each variant is built from the working tree's csrc with its -D flags into /tmp/libsrbd_mpc_<NAME>.so;
 the variants then run bench.py (--steps 50, SRBD_LIB) in turn, R rounds, and the fused kernel's
 HIP-event time per launch is printed per run and as the per-variant median.
@@ -19,6 +19,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--horizon", type=int, default=10)
     p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--batch", type=int, default=4096)
     p.add_argument("variants", nargs="+")
     a = p.parse_args()
     libs = {}
@@ -33,7 +34,8 @@ def main():
     for _ in range(a.rounds):
         for name, lib in libs.items():
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "50", "--warmup", "10",
-                                "--no-cpu-baseline", "--horizon", str(a.horizon)],
+                                "--no-cpu-baseline", "--horizon", str(a.horizon),
+                                "--batch-per-gpu", str(a.batch)],
                                env={**os.environ, "SRBD_LIB": lib}, capture_output=True, text=True, timeout=300)
             if r.returncode:
                 raise SystemExit(f"{name}: bench failed\n{r.stderr[-2000:]}")
