@@ -261,6 +261,38 @@ def test_ragged_batches(N, B):
     assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
 
 
+@pytest.mark.parametrize("N,B,random_gait", [(10, 4096, False), (20, 4096, False), (10, 8192, False),
+                                              (10, 4096, True)])
+def test_full_size_properties(N, B, random_gait):
+    """BASELINE configs 2-5 at their full per-GPU sizes, through size-independent properties:
+    a QP's solution does not depend on its batch position or the batch size (a permuted batch and
+    a sub-batch reproduce the same rows bit for bit), every iterate is finite and strictly
+    interior, the barrier parameter fell below its cold-start value in every env (s0 = max(d, 1),
+    z0 = 1, so mu0 >= 1), and a strided sample of 64 envs matches the oracle at the K = 10
+    tolerances."""
+    K = 10
+    wl = make_workload(B, N, seed=7000 + B + N, random_gait=random_gait, residuals=random_gait)
+    ins = _cuda(wl.inputs)
+    full = [t.clone() for t in solver.mpc_solve(ins, N, K, y0=1.0)]
+    perm = torch.randperm(B, generator=torch.Generator().manual_seed(B + N)).cuda()
+    permuted = [t.clone() for t in solver.mpc_solve([t[perm].contiguous() for t in ins], N, K, y0=1.0)]
+    head = solver.mpc_solve([t[:B // 8].contiguous() for t in ins], N, K, y0=1.0)
+    torch.cuda.synchronize()
+    for a, p, h in zip(full, permuted, head):
+        assert torch.equal(a[perm], p)
+        assert torch.equal(a[:B // 8], h)
+    x, s, z, y, res, mu = [t.cpu().numpy() for t in full]
+    for v in (x, s, z, y, res, mu):
+        assert np.all(np.isfinite(v))
+    assert s.min() > 0.0 and z.min() > 0.0
+    assert mu.max() < 1.0, f"barrier parameter did not fall in every env: max mu {mu.max():.3e}"
+    idx = np.arange(0, B, B // 64)
+    ref = oracle.mpc_solve(N, K, [np.ascontiguousarray(a[idx]) for a in wl.inputs], y0=1.0)
+    u_gpu, u_ref = x[idx, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
+    assert rel_err_rows(u_gpu, u_ref).max() <= U0_TOL
+    assert rel_err_rows(x[idx], ref[0]).max() <= dict(SOLVER_CASES)[K]
+
+
 def test_empty_batch_is_a_no_op():
     N = 10
     wl = make_workload(1, N, seed=1)
