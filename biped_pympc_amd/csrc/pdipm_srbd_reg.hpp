@@ -1158,7 +1158,24 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   const double* RXu = smem + Lo::RXu;
   PROF_MARK_CTX(C);
   const int n_iter = kFused ? fa.n_iter : args.n_iter;
+#ifdef SRBD_CHAIN_PRIO  // A/B experiment: progress halves (2 / 0) and +1 inside the block chains
+  auto setp = [](int l) {
+    if (l >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (l == 2) __builtin_amdgcn_s_setprio(2);
+    else if (l == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+#endif
   for (int it = 0; it < n_iter; ++it) {
+#ifdef SRBD_CHAIN_PRIO
+    const int plvl = (2 * it < n_iter) ? 2 : 0;
+    setp(plvl);
+#define SRBD_CHAIN_UP() setp(plvl + 1)
+#define SRBD_CHAIN_DOWN() setp(plvl)
+#else
+#define SRBD_CHAIN_UP()
+#define SRBD_CHAIN_DOWN()
+#endif
     if constexpr (TPB == 64 && SRBD_PROGRESS_PRIO) {
       // Wave priority falls with this QP's progress (3 over the first quarter of the iterations, 0
       // over the last): of the two waves sharing a SIMD the one further behind issues first, so
@@ -1182,11 +1199,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #endif
     C.factor_build();
     C.solve_rhs(0, 0.0);
+    SRBD_CHAIN_UP();
     C.template factor_chain<true>();  // + the affine forward elimination
 #ifdef SRBD_REPEAT_PHASE
     if (SRBD_REPEAT_PHASE == 3) C.solve(0, 0.0);
 #endif
     C.template solve_chain<true>();
+    SRBD_CHAIN_DOWN();
     C.solve_finish();
     const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
     double sza = 0.0;
@@ -1199,7 +1218,15 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
     __syncthreads();
     PROF_ADD_CTX(C, 5);
-    C.solve(1, sigma * mu * 1.0);
+#ifdef SRBD_CHAIN_PRIO
+    C.solve_rhs(1, sigma * mu * 1.0);  // C.solve(1, ...) with its chain phase bracketed
+    SRBD_CHAIN_UP();
+    C.template solve_chain<false>();
+    SRBD_CHAIN_DOWN();
+    C.solve_finish();
+#else
+    C.solve(1, sigma * mu * 1.0);  // (spelling the three phases out here costs N = 20 58 more spills)
+#endif
     const double apc = C.step_length(C.s, C.ds), adc = C.step_length(C.z, C.dz);
     __syncthreads();
     double szn = 0.0;
@@ -1237,6 +1264,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     __syncthreads();
     PROF_ADD_CTX(C, 5);
   }
+#undef SRBD_CHAIN_UP
+#undef SRBD_CHAIN_DOWN
   PROF_FLUSH(C);
   auto outp = [&](int k) { return kFused ? fa.out[k] : solver_out(args, k); };
   double* xo = outp(0) + (size_t)env * nz;

@@ -242,13 +242,19 @@ __device__ unsigned long long g_phase_cycles[16];
 #define PROF_FLUSH(ctx)
 #endif
 
-// 1/d: v_rcp_f64 (~2^-24 relative) refined by one cubically convergent step y (1 + e + e^2),
-// e = 1 - d y: three dependent FMAs instead of two Newton steps' four; correctly rounded on 4M
-// log-uniform samples (scripts/microbench_fp64.hip), about a third of an IEEE division's cost
+// 1/d: v_rcp_f64 (~2^-24 relative) refined by one Newton step y (1 + e), e = 1 - d y: relative
+// error ~2^-46 (not always correctly rounded), two dependent FMAs. The cubic step y (1 + e + e^2)
+// (-DSRBD_RCP_CUBIC) is correctly rounded on 4M log-uniform samples (scripts/microbench_fp64.hip)
+// for one FMA more; the Newton step measured -0.6 % (N = 10) / -1.4 % (N = 20) on the fused step
+// with oracle parity unchanged in magnitude (profiles/r01/rcp_variants.txt)
 __device__ __forceinline__ double rcp3(double d) {
   const double y = __builtin_amdgcn_rcp(d);
   const double e = fma(-d, y, 1.0);
+#ifdef SRBD_RCP_CUBIC
   return fma(y, fma(e, e, e), y);
+#else
+  return fma(y, e, y);
+#endif
 }
 
 // ------------------------------------------------------------------ wave64 reductions ----
