@@ -80,11 +80,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))]
     srcs.append(os.path.join(INCLUDE, "srbd_mpc.h"))
     if force or not _newer(core, srcs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-o", core, os.path.join(CSRC, "srbd_mpc.hip")]
-        if verbose:
-            print(" ".join(cmd))
-        _run(cmd)
+        # the N = 20 register kernels in their own unit, scheduled with the register-pressure
+        # trackers (csrc/reg20.hpp), linked into the same library
+        obj20 = os.path.join(LIB_DIR, "srbd_reg20.o")
+        obj_main = os.path.join(LIB_DIR, "srbd_mpc.o")
+        cmds = [[HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+                 "-mllvm", "-amdgpu-use-amdgpu-trackers=1", "-o", obj20, os.path.join(CSRC, "srbd_reg20.hip")],
+                [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-DSRBD_SPLIT_REG20",
+                 "-o", obj_main, os.path.join(CSRC, "srbd_mpc.hip")],
+                [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", core, obj_main, obj20]]
+        for cmd in cmds:
+            if verbose:
+                print(" ".join(cmd))
+            _run(cmd)
     for fn, N, K in DROPIN_CONFIGS:
         _build_dropin_lib(fn, N, K, core, force, verbose)
     return core

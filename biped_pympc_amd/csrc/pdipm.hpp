@@ -508,6 +508,7 @@ struct SolverCtx {
   }
 };
 
+#ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again
 __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = blockIdx.x;
@@ -620,5 +621,6 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
     mo[0] = mu_new;
   }
 }
+#endif  // SRBD_NO_GENERAL_KERNEL
 
 }  // namespace srbd

@@ -1,6 +1,8 @@
 // srbd_mpc.hip -- libsrbd_mpc.so: HIP kernels (gfx950) + the C-ABI of include/srbd_mpc.h.
 //
-// One translation unit so the constant-memory pattern tables (srbd_common.hpp) exist once.
+// The main translation unit; the N = 20 register kernels are built apart in srbd_reg20.hip when
+// SRBD_SPLIT_REG20 is defined (the product build, biped_pympc_amd/build.py). The constant-memory
+// tables (srbd_common.hpp) are compile-time initialised, so each unit's copy is identical.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -15,6 +17,7 @@
 #include "pdipm_srbd_reg.hpp"
 #include "qp_former.hpp"
 #include "mpc_io.hpp"
+#include "reg20.hpp"
 
 namespace {
 
@@ -71,8 +74,13 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
       if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, &cfg_reg10)) return rc;
       hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
     } else {
+#ifdef SRBD_SPLIT_REG20
+      if (int rc = ensure_lds_attr(srbd::reg20::solver_kernel(), kRegLds20, &cfg_reg20)) return rc;
+      srbd::reg20::launch_solver(a, kRegLds20, s);
+#else
       if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, &cfg_reg20)) return rc;
       hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, s, a);
+#endif
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
@@ -293,8 +301,13 @@ int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const do
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, &cfg10)) return rc;
     hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(batch), dim3(64), kRegLds10, st, a);
   } else {
+#ifdef SRBD_SPLIT_REG20
+    if (int rc = ensure_lds_attr(srbd::reg20::step_kernel(), kRegLds20, &cfg20)) return rc;
+    srbd::reg20::launch_step(a, kRegLds20, st);
+#else
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, &cfg20)) return rc;
     hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(batch), dim3(srbd::reg_tpb(20)), kRegLds20, st, a);
+#endif
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");
