@@ -103,6 +103,7 @@ struct SolverCtx {
   double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,
       *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
+  double *xsg, *ysg;  // this QP's x / y output rows: the saved dx / dy during the refinement solve
 
   // ---- structured access to the CCS values (stage-periodic tables) ----
   __device__ double Pv(int i, int r) const { return AV[a_pidx(c_tab, N, i, r)]; }
@@ -327,16 +328,76 @@ struct SolverCtx {
     }
   }
 
+  // One step of iterative refinement of the combined direction (derivation at pdipm_srbd_reg.hpp
+  // RegCtx::refine_rhs): RX <- RX + (H + beta) dx + G^T dz + A^T dy, RE <- RE + A dx - delta dy
+  // (minus the residual of KKT rows 1 and 4; rows 2 and 3 hold by construction), dx and dy saved
+  // to the output rows for solve(true).
+  __device__ void refine_rhs() {
+    for (int e = lane; e < nz; e += 64) xsg[e] = TV[e];
+    for (int e = lane; e < p; e += 64) ysg[e] = DY[e];
+    for (int c = lane; c < nz; c += 64) {
+      double v = (HV[c] + kBeta) * TV[c] + RX[c];
+      if (c >= 12 * N) {
+        const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
+        double gz = 0.0;
+        for (int q = 0; q < 28; ++q)
+          if (c_tab.gcol[q] == j) gz += G(i, q) * DZ[16 * i + c_tab.grow[q]];
+        double ay = 0.0;
+        const int ub = a_ublock(N, i) + c_tab.cpu[j];
+        for (int t = 0; t < c_tab.su_n[j]; ++t) ay += AV[ub + t] * DY[12 * i + c_tab.su[j][t]];
+        if (j == 6) ay += AV[ub + c_tab.su_n[j]] * DY[12 * N + 2 * i];
+        if (j == 9) ay += AV[ub + c_tab.su_n[j]] * DY[12 * N + 2 * i + 1];
+        v = (v + gz) + ay;
+      } else {
+        const int k = c / 12 + 1, j = c % 12;
+        double ay;
+        if (k < N) {
+          const int xb = a_xblock(k) + c_tab.cpx[j];
+          ay = AV[xb] * DY[12 * (k - 1) + j];
+          for (int t = 0; t < c_tab.sx_n[j]; ++t) ay += AV[xb + 1 + t] * DY[12 * k + c_tab.sx[j][t]];
+        } else {
+          ay = AV[36 * (N - 1) + j] * DY[12 * (k - 1) + j];
+        }
+        v = v + ay;
+      }
+      RX[c] = v;
+    }
+    for (int e = lane; e < p; e += 64) {
+      double v = 0.0;
+      if (e < 12 * N) {
+        const int i = e / 12, r = e % 12;
+        if (i >= 1)
+          for (int j = 0; j < 12; ++j) {
+            const int o = c_tab.Mi[r][j];
+            if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
+          }
+        v += Pv(i, r) * TV[12 * i + r];
+        for (int j = 0; j < 12; ++j) {
+          const int o = c_tab.Ni[r][j];
+          if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
+        }
+      } else {
+        const int i = (e - 12 * N) / 2, w = (e - 12 * N) % 2;
+        v = (w == 0 ? E6(i) * TV[12 * N + 12 * i + 6] : E9(i) * TV[12 * N + 12 * i + 9]);
+      }
+      RE[e] = (v + RE[e]) - kDelta * DY[e];
+    }
+    __syncthreads();
+  }
+
   // ------------------------------------------------------------------------- solve ----
   // Solves K [dx; ds; dz; dy] = [-RX; R2; -RS; -RE] with the current factors.
   // Result: dx -> TV, ds -> DS, dz -> DZ, dy -> DY.
-  __device__ void solve() {
-    for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
+  // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV kept from the
+  // combined solve), then dx = saved + correction before dz, ds are formed; DY is the correction.
+  __device__ void solve(bool ref = false) {
+    if (!ref)
+      for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
     __syncthreads();
     // r1~ = r1 - G^T VV
     for (int c = lane; c < nz; c += 64) {
       double v = -RX[c];
-      if (c >= 12 * N) {
+      if (c >= 12 * N && !ref) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double g = 0.0;
         for (int q = 0; q < 28; ++q)
@@ -440,7 +501,7 @@ struct SolverCtx {
       } else {
         aty = AV[36 * (N - 1) + j] * QV[12 * (k - 1) + j];
       }
-      TV[c] = TV[c] - aty / phix(k, j);
+      TV[c] = ref ? xsg[c] + (TV[c] - aty / phix(k, j)) : TV[c] - aty / phix(k, j);
     }
     for (int task = lane; task < 3 * N; task += 64) {
       // u columns: per (stage, foot) block or per stage scalars
@@ -464,16 +525,19 @@ struct SolverCtx {
           double t = 0.0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
-          TV[b + c_tab.foot_col[f][a]] -= t;
+          const int o = b + c_tab.foot_col[f][a];
+          TV[o] = ref ? xsg[o] + (TV[o] - t) : TV[o] - t;
         }
       } else {
         const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
         const double a6 = aty_u(6), a9 = aty_u(9), a8 = aty_u(8), a11 = aty_u(11);
-        TV[b + 6] -= PH[24 * i + 20] * a6;
-        TV[b + 9] -= PH[24 * i + 21] * a9;
-        TV[b + 8] -= PH[24 * i + 22] * a8;
-        TV[b + 11] -= PH[24 * i + 23] * a11;
+        const double t6 = TV[b + 6] - PH[24 * i + 20] * a6, t9 = TV[b + 9] - PH[24 * i + 21] * a9;
+        const double t8 = TV[b + 8] - PH[24 * i + 22] * a8, t11 = TV[b + 11] - PH[24 * i + 23] * a11;
+        TV[b + 6] = ref ? xsg[b + 6] + t6 : t6;
+        TV[b + 9] = ref ? xsg[b + 9] + t9 : t9;
+        TV[b + 8] = ref ? xsg[b + 8] + t8 : t8;
+        TV[b + 11] = ref ? xsg[b + 11] + t11 : t11;
         const double rho6 = R1T[b + 6] - a6, rho9 = R1T[b + 9] - a9;
         DY[12 * N + 2 * i] = (e6 * rho6 - p6 * r4a) / (p6 * kDelta + e6 * e6);
         DY[12 * N + 2 * i + 1] = (e9 * rho9 - p9 * r4b) / (p9 * kDelta + e9 * e9);
@@ -540,6 +604,8 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   C.fg = solver_in(args, 3) + (size_t)env * nz;
   C.hg = solver_in(args, 4) + (size_t)env * m;
   C.bg = solver_in(args, 5) + (size_t)env * p;
+  C.xsg = solver_out(args, 0) + (size_t)env * nz;
+  C.ysg = solver_out(args, 3) + (size_t)env * p;
   for (int e = lane; e < nA; e += 64) C.AV[e] = Ag[e];
   for (int e = lane; e < nG; e += 64) C.GV[e] = Gg[e];
   for (int e = lane; e < nz; e += 64) C.HV[e] = Hg[e];
@@ -562,6 +628,15 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
   for (int it = 0; it < args.n_iter; ++it) {
     const double mu = C.residuals();
+    if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
+      double a = 0.0, b = 0.0, c = 0.0;
+      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
+      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
+      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
+      res0 = sqrt(wave_sum(a));
+      res1 = sqrt(wave_sum(b));
+      res2 = sqrt(wave_sum(c));
+    }
     C.factor();
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
@@ -580,6 +655,8 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
     }
     __syncthreads();
     C.solve();
+    C.refine_rhs();
+    C.solve(true);
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
     __syncthreads();
     double szn = 0.0;
@@ -591,17 +668,8 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
       C.Z[q] = zn;
       szn += sn * zn;
     }
-    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * C.DY[e];
+    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
     mu_new = wave_sum(szn) / m;
-    if (it == args.n_iter - 1) {
-      double a = 0.0, b = 0.0, c = 0.0;
-      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
-      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
-      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
-      res0 = sqrt(wave_sum(a));
-      res1 = sqrt(wave_sum(b));
-      res2 = sqrt(wave_sum(c));
-    }
     __syncthreads();
   }
   double* xo = solver_out(args, 0) + (size_t)env * nz;

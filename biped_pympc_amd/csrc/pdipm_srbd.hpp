@@ -69,11 +69,7 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
 // entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
 // block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
-#ifdef SRBD_EXP_NODPP  // timing experiment only (wrong results): plain FMAs, no broadcast
-#define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64 " D ", " S ", " C "\n"
-#else
 #define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
-#endif
 
 // one Gauss-Jordan pivot update: S[j] -= S[j](lane K) * t for the 11 columns j != K (the caller
 // overwrites S[K]); row_newbcast needs K at compile time, hence one asm block per K
@@ -139,31 +135,9 @@ struct PivotLanes {  // s_and_saveexec_b64 literal (32-bit, sign-extended; lanes
   static constexpr int64_t value = (int32_t)(m16 | (m16 << 16));
 };
 
-#ifdef SRBD_EXP_GJ_NODEP  // timing experiment only (wrong results): pivots read the input block,
-                          // which removes the pivot-to-pivot dependency and keeps the work
-#endif
 template <int K>
-__device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc
-#ifdef SRBD_EXP_GJ_NODEP
-                                         , const double (&g_exp_s0_reg)[12]
-#endif
-) {
-#ifdef SRBD_EXP_GJ_NODEP
-  const double pk = bc16(g_exp_s0_reg[K], K);
-#else
+__device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc) {
   const double pk = bc16(Sr[K], K);
-#endif
-#ifdef SRBD_GJ_SELECT  // pivot-lane special cases as selects on a lane compare (no EXEC writes)
-  const int l16 = __lane_id() & 15;
-  const bool piv = K == 11 ? l16 >= 11 : l16 == K;
-  Sr[K] = piv ? 0.0 : Sr[K];
-  const double id = rcp3(pk);
-  const double t = Sr[K] * id;  // 0 on the pivot lanes
-  pivot_update(Sr, t, K);
-  Sr[K] = piv ? -1.0 : t;
-  sc = piv ? id : sc;
-  if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
-#else
   uint64_t sv;
   asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], 0\n\ts_mov_b64 exec, %[sv]"
       : [x] "+v"(Sr[K]), [sv] "=&s"(sv)
@@ -175,24 +149,12 @@ __device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc
   asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], -1.0\n\tv_mov_b64 %[s], %[id]\n\ts_mov_b64 exec, %[sv]"
       : [x] "+v"(Sr[K]), [s] "+v"(sc), [sv] "=&s"(sv)
       : [id] "v"(id), [m] "n"(PivotLanes<K>::value));
-#ifdef SRBD_EXP_GJ_NODEP
-  if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc, g_exp_s0_reg);
-#else
   if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
-#endif
-#endif  // SRBD_GJ_SELECT
 }
 
 __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], double (&Dr)[12]) {
   double sc = 1.0;
-#ifdef SRBD_EXP_GJ_NODEP
-  double s0[12];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) s0[j] = Sr[j];
-  gj_pivot<0>(Sr, sc, s0);
-#else
   gj_pivot<0>(Sr, sc);
-#endif
   // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale
   const double nsc = -sc;
 #pragma unroll
@@ -213,6 +175,7 @@ struct FastCtx {
   double *Md, *Nd, *Cd, *Gd, *K0, *K1, *Pd, *IX, *Hu, *SG, *PH, *DV, *X, *S, *Z, *Y, *RX, *RS, *RE, *WD,
       *DI, *VV, *TV, *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
+  double *xsg, *ysg;  // this QP's x / y output rows: the saved dx / dy during the refinement solve
   PROF_DECL
   // Hu: [H_u (12) | H_x (12)] ; SG: [gamma6, psi8, gamma9, psi11, phi6, phi9, e6, e9]
 
@@ -448,16 +411,65 @@ struct FastCtx {
     PROF_ADD(2);
   }
 
+  // One step of iterative refinement of the combined direction (pdipm_srbd_reg.hpp RegCtx::refine_rhs
+  // has the derivation): r_x <- r_x + (H + beta) dx + G^T dz + A^T dy, r_e <- r_e + A dx - delta dy,
+  // i.e. minus the residual of KKT rows 1 and 4; dx, dy saved to the output rows for solve(2).
+  __device__ void refine_rhs() {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    (void)m;
+    for (int e = lane; e < nz; e += 64) xsg[e] = TV[e];
+    for (int e = lane; e < p; e += 64) ysg[e] = DY[e];
+    for (int c = lane; c < nz; c += 64) {
+      double v;
+      if (c < 12 * N) {
+        const int k = c / 12 + 1, j = c % 12;
+        v = (Hu[12 + j] + kBeta) * TV[c] + RX[c];
+        double ay = Pd[j] * DY[12 * (k - 1) + j];
+        if (k < N) ay += dotcol12(Md, j, DY + 12 * k);
+        v = v + ay;
+      } else {
+        const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
+        v = (Hu[j] + kBeta) * TV[c] + RX[c];
+        double gz = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gz += Gd[k * 12 + j] * DZ[16 * i + k];
+        double ay = dotcol12(Nd, j, DY + 12 * i);
+        if (j == 6) ay += SG[6] * DY[12 * N + 2 * i];
+        if (j == 9) ay += SG[7] * DY[12 * N + 2 * i + 1];
+        v = (v + gz) + ay;
+      }
+      RX[c] = v;
+    }
+    for (int e = lane; e < p; e += 64) {
+      double v;
+      if (e < 12 * N) {
+        const int i = e / 12, r = e % 12;
+        v = (i >= 1) ? dotrow12(Md + 12 * r, TV + 12 * (i - 1)) : 0.0;
+        v += Pd[r] * TV[12 * i + r];
+        v += dotrow12(Nd + 12 * r, TV + 12 * N + 12 * i);
+      } else {
+        const int i = (e - 12 * N) / 2, w = (e - 12 * N) % 2;
+        v = SG[6 + w] * TV[12 * N + 12 * i + (w ? 9 : 6)];
+      }
+      RE[e] = (v + RE[e]) - kDelta * DY[e];
+    }
+    __syncthreads();
+  }
+
   // ------------------------------------------------------------------------ solve ----
-  // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
+  // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu);
+  // mode 2: the refinement solve (rhs from refine_rhs, VV kept from mode 1, dx = saved + correction)
   __device__ void solve(int mode, double smu) {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
     (void)nz; (void)m; (void)p;
-    for (int q = lane; q < m; q += 64) {
-      const double si = 1.0 / S[q];
-      double r2 = -(si * (S[q] * Z[q]));
-      if (mode) r2 = r2 + -(si * (S[q] * Z[q] + DS[q] * DZ[q] - smu));
-      VV[q] = DI[q] * (r2 + WD[q] * RS[q]);
+    const bool ref = mode == 2;
+    if (!ref) {
+      for (int q = lane; q < m; q += 64) {
+        const double si = 1.0 / S[q];
+        double r2 = -(si * (S[q] * Z[q]));
+        if (mode) r2 = r2 + -(si * (S[q] * Z[q] + DS[q] * DZ[q] - smu));
+        VV[q] = DI[q] * (r2 + WD[q] * RS[q]);
+      }
     }
     __syncthreads();
     // t = Phi^-1 r1~ with r1~ = -RX - G^T VV; G only touches the foot columns {0,1,2,7 | 3,4,5,10},
@@ -473,8 +485,10 @@ struct FastCtx {
         for (int a = 0; a < 4; ++a) {
           const int col = c_tab.foot_col[f][a];
           double gv = 0.0;
+          if (!ref) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) gv += Gd[(8 * f + k) * 12 + col] * vv[k];
+            for (int k = 0; k < 8; ++k) gv += Gd[(8 * f + k) * 12 + col] * vv[k];
+          }
           rv[a] = -RX[b + col] - gv;
         }
 #pragma unroll
@@ -604,7 +618,7 @@ struct FastCtx {
       const int k = c / 12 + 1, j = c % 12;
       double aty = Pd[j] * QV[12 * (k - 1) + j];
       if (k < N) aty += dotcol12(Md, j, QV + 12 * k);
-      TV[c] = TV[c] - aty * IX[j];
+      TV[c] = ref ? xsg[c] + (TV[c] - aty * IX[j]) : TV[c] - aty * IX[j];
     }
     for (int task = lane; task < 3 * N; task += 64) {
       const bool foot = task < 2 * N;
@@ -622,16 +636,17 @@ struct FastCtx {
           double t = 0.0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
-          TV[b + c_tab.foot_col[f][a]] -= t;
+          const int o = b + c_tab.foot_col[f][a];
+          TV[o] = ref ? xsg[o] + (TV[o] - t) : TV[o] - t;
         }
       } else {
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
         const double a6 = dotcol12(Nd, 6, yi), a9 = dotcol12(Nd, 9, yi);
         const double a8 = dotcol12(Nd, 8, yi), a11 = dotcol12(Nd, 11, yi);
-        TV[b + 6] -= SG[0] * a6;
-        TV[b + 9] -= SG[2] * a9;
-        TV[b + 8] -= SG[1] * a8;
-        TV[b + 11] -= SG[3] * a11;
+        TV[b + 6] = ref ? xsg[b + 6] + (TV[b + 6] - SG[0] * a6) : TV[b + 6] - SG[0] * a6;
+        TV[b + 9] = ref ? xsg[b + 9] + (TV[b + 9] - SG[2] * a9) : TV[b + 9] - SG[2] * a9;
+        TV[b + 8] = ref ? xsg[b + 8] + (TV[b + 8] - SG[1] * a8) : TV[b + 8] - SG[1] * a8;
+        TV[b + 11] = ref ? xsg[b + 11] + (TV[b + 11] - SG[3] * a11) : TV[b + 11] - SG[3] * a11;
         const double rho6 = -RX[b + 6] - a6, rho9 = -RX[b + 9] - a9;  // no G entries in cols 6, 9
         DY[12 * N + 2 * i] = (SG[6] * rho6 - SG[4] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
         DY[12 * N + 2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
@@ -688,6 +703,8 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   C.fg = solver_in(args, 3) + (size_t)env * nz;
   C.hg = solver_in(args, 4) + (size_t)env * m;
   C.bg = solver_in(args, 5) + (size_t)env * p;
+  C.xsg = solver_out(args, 0) + (size_t)env * nz;
+  C.ysg = solver_out(args, 3) + (size_t)env * p;
 
   // ---- compact load: stage-0/1 slices in dense form ----
   for (int e = lane; e < 144; e += 64) {
@@ -774,6 +791,15 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   PROF_MARK_CTX(C);
   for (int it = 0; it < args.n_iter; ++it) {
     const double mu = C.residuals();
+    if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
+      double a = 0.0, b = 0.0, c = 0.0;
+      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
+      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
+      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
+      res0 = sqrt(wave_sum(a));
+      res1 = sqrt(wave_sum(b));
+      res2 = sqrt(wave_sum(c));
+    }
     PROF_ADD_CTX(C, 0);
     C.factor();
     C.solve(0, 0.0);
@@ -785,6 +811,8 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
     __syncthreads();
     PROF_ADD_CTX(C, 5);
     C.solve(1, sigma * mu * 1.0);
+    C.refine_rhs();
+    C.solve(2, 0.0);
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
     __syncthreads();
     double szn = 0.0;
@@ -796,17 +824,8 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
       C.Z[q] = zn;
       szn += sn * zn;
     }
-    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * C.DY[e];
+    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
     mu_new = wave_sum(szn) / m;
-    if (it == args.n_iter - 1) {
-      double a = 0.0, b = 0.0, c = 0.0;
-      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
-      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
-      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
-      res0 = sqrt(wave_sum(a));
-      res1 = sqrt(wave_sum(b));
-      res2 = sqrt(wave_sum(c));
-    }
     __syncthreads();
     PROF_ADD_CTX(C, 5);
   }

@@ -325,6 +325,10 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
+  // this QP's output rows of x and y: while the refinement solve runs they hold the first solve's
+  // dx and dy (the LDS has no room for a second direction; each element is written and re-read by
+  // the same lane, and the final iterate overwrites both rows at the end)
+  double *xsg, *ysg;
   PROF_DECL
 
   __device__ double* at(int off) const { return L + off; }
@@ -620,11 +624,7 @@ struct RegCtx {
 #pragma unroll
             for (int c = 0; c < 12; ++c) Sr[c] = dv_at(DV, offs[c], imm);
           }
-#ifdef SRBD_EXP_NOSCHUR  // timing experiment only (wrong results): no Schur update
-          if (false) {
-#else
           if (prev) {
-#endif
             double V[12];
             // V[c] = sum_k Dr[k] C[c][k]: row c of C is lane c's own coupling row (crd, cra*, crb),
             // broadcast inside the FMAs (row_newbcast:c) instead of re-read from LDS every step
@@ -658,12 +658,7 @@ struct RegCtx {
           }
         }
         if (act && !(mstep && g == 1)) {
-#ifdef SRBD_EXP_NOINV  // timing experiment only (wrong results): no block inverse
-#pragma unroll
-          for (int c = 0; c < 12; ++c) Dr[c] = Sr[c];
-#else
           inverse_rows12(Sr, Dr);
-#endif
           // every lane writes its whole row: (r, c) and (c, r) share a packed slot, so each slot is
           // written twice with the two (rounding-different) halves of the symmetric inverse; the
           // later ds_write in program order wins, deterministically (shadow lanes 12..15 repeat row
@@ -689,30 +684,124 @@ struct RegCtx {
   }
 
   // ------------------------------------------------------------------------ solve ----
-  // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu)
+  // kMode 0: affine rhs r2 = -(S^-1 (s o z)); 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu);
+  // 2: refinement -- the right-hand side is the residual of KKT rows 1 and 4 left in r_x / r_e by
+  // refine_rhs(), rows 2 and 3 have none (VV keeps the combined solve's D^-1 (r2 - W r3)).
   // One solve = solve_rhs (t = Phi^-1 r~ and the dual right-hand side g, in QV) -> solve_chain
   // (the twisted block forward elimination and back substitution: dy in QV) -> solve_finish (dx,
   // dz, ds). The affine solve's forward elimination runs inside factor_chain<true> instead, with
   // each block's inverse still in registers (solve_chain<true> then only substitutes back).
-  __device__ void solve(int mode, double smu) {
-    solve_rhs(mode, smu);
+  template <int kMode>
+  __device__ void solve(double smu) {
+    solve_rhs<kMode>(smu);
     solve_chain<false>();
-    solve_finish();
+    solve_finish<kMode == 2>();
   }
 
-  SRBD_PHASE_ATTR __device__ void solve_rhs(int mode, double smu) {
+  // One step of iterative refinement of the combined direction d = (dx, ds, dz, dy). The dual
+  // Schur elimination applies explicit inverses of the 12x12 blocks, whose error is not
+  // backward-stable: along the stiff directions of S (the yaw-moment columns enter S_ii with
+  // 1/(R + beta) = 1e4) dy is off by ~eps cond |dy|, and dx_u = Phi_u^-1 (r - N^T dy) multiplies
+  // that by 1e4 (profiles/r02/refinement_parity.txt: 1e-7 relative in x after one iteration against
+  // the oracle's sparse LDL^T, 1e-12 after this step). The residual of the full KKT of
+  // sparse_pdipm_solver.py:412-439 for d is zero in rows 2 and 3 by construction (ds, dz come from
+  // them), so only rows 1 and 4 are formed:
+  //   e1 = -r_x - (H + beta I) dx - G^T dz - A^T dy,   e4 = -r_e - A dx + delta dy,
+  // left as r_x <- -e1, r_e <- -e4 for solve<2>, whose result is added to the saved d.
+  SRBD_PHASE_ATTR __device__ void refine_rhs() {
+    const int lane = fresh_lane();
+    const double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm), *Mc = at(Lo::Mc),
+                 *Nd = at(Lo::Nd), *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
+    double *Zd = at(Lo::Z), *RXu = at(Lo::RXu), *REm = at(Lo::REm);
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // dz to LDS for G^T dz (Z's z mirror is dead until the update)
+      const int q = lane + TPB * t;
+      if (q < m) Zd[q] = dz[t];
+    }
+#pragma unroll
+    for (int t = 0; t < (nz + TPB - 1) / TPB; ++t) {  // save dx, dy (owner lanes, see xsg)
+      const int e = lane + TPB * t;
+      if (e < nz) xsg[e] = TV[e];
+      if (e < p) ysg[e] = e < nx ? QV[e] : DYm[e - nx];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // x columns: (H_x + beta) dx + r_x + P dy_{k-1} + M^T dy_k
+      const int c = lane + TPB * t;
+      if (c < nx) {
+        const int k = c / 12 + 1, j = c % 12;
+        const double v = (Hu[12 + j] + kBeta) * TV[c] + rxx[t];
+        double ay = Pd[j] * QV[12 * (k - 1) + j];
+        if (k < N) ay += mcol(Mc, j, QV + 12 * k);
+        rxx[t] = v + ay;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // u columns: (H_u + beta) du + r_x + G^T dz + N^T dy + e-rows
+      const int c = lane + TPB * t;
+      if (c < nx) {
+        const int i = c / 12, j = c % 12;
+        const double v = (Hu[j] + kBeta) * TV[nx + c] + RXu[c];
+        double gz = 0.0;
+        const int f = foot_of(j);
+        if (f >= 0) {
+          const int a = foot_pos(j);
+          const double* zf = Zd + 16 * i + 8 * f;
+          const double* g = Gf + 32 * f + a;
+          double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            g0 += g[4 * k] * zf[k];
+            g1 += g[4 * (k + 4)] * zf[k + 4];
+          }
+          gz = g0 + g1;
+        }
+        double ay = ncol(Nd, j, QV + 12 * i, j % 3);
+        if (j == 6) ay += SG[6] * DYm[2 * i];
+        if (j == 9) ay += SG[7] * DYm[2 * i + 1];
+        RXu[c] = (v + gz) + ay;
+      }
+    }
+    re_refine<0>(TV, QV, Mc, Pd, Nd);
+    re_refine<1>(TV, QV, Mc, Pd, Nd);
+    {
+      const ERow q = erow(lane, 2);
+      if (q.valid) {
+        const int w = q.r;
+        re[2] = (SG[6 + w] * TV[nx + 12 * q.i + (w ? 9 : 6)] + re[2]) - kDelta * DYm[q.e - nx];
+        REm[q.e - nx] = re[2];
+      }
+    }
+    __syncthreads();
+  }
+  template <int t>
+  __device__ void re_refine(const double* TV, const double* QV, const double* Mc, const double* Pd,
+                            const double* Nd) {  // r_e <- A dx + r_e - delta dy (dynamics rows)
+    const ERow q = erow(fresh_lane(), t);
+    if (q.valid) {
+      double v = (q.i >= 1) ? mrow(Mc, q.r, TV + 12 * (q.i - 1)) : 0.0;
+      v += Pd[q.r] * TV[12 * q.i + q.r];
+      v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
+      re[t] = (v + re[t]) - kDelta * QV[q.e];
+    }
+  }
+
+  template <int kMode>
+  SRBD_PHASE_ATTR __device__ void solve_rhs(double smu) {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
                  *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd);
+    if constexpr (kMode != 2) {
 #pragma unroll
-    for (int t = 0; t < SI; ++t) {
-      const int q = lane + TPB * t;
-      if (q < m) {
-        const double si = rcp3(s[t]);
-        double r2 = -(si * (s[t] * z[t]));
-        if (mode) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
-        VV[q] = di[t] * (r2 + wd[t] * rs[t]);
+      for (int t = 0; t < SI; ++t) {
+        const int q = lane + TPB * t;
+        if (q < m) {
+          const double si = rcp3(s[t]);
+          double r2 = -(si * (s[t] * z[t]));
+          if (kMode == 1) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
+          VV[q] = di[t] * (r2 + wd[t] * rs[t]);
+        }
       }
     }
 #pragma unroll
@@ -725,25 +814,30 @@ struct RegCtx {
     if (lane < 3 * N) {
       if (lane < 2 * N) {
         const int i = lane >> 1, f = lane & 1, b = 12 * i;
-        const double* vv = VV + 16 * i + 8 * f;
         double rv[4];
-        const double* g = Gf + 32 * f;  // (G^T vv)_a over column a's structural rows
-        double vk[8];
+        if constexpr (kMode == 2) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) vk[k] = vv[k];
-        const double gfx = g[0] * vk[0] + g[4] * vk[1];
-        const double gfy = g[9] * vk[2] + g[13] * vk[3];
-        const double gmy = g[19] * vk[4] + g[23] * vk[5];
-        double gz0 = 0.0, gz1 = 0.0;
+          for (int a = 0; a < 4; ++a) rv[a] = -RXu[b + foot_colj(f, a)];
+        } else {
+          const double* vv = VV + 16 * i + 8 * f;
+          const double* g = Gf + 32 * f;  // (G^T vv)_a over column a's structural rows
+          double vk[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          gz0 += g[4 * k + 2] * vk[k];
-          gz1 += g[4 * (k + 4) + 2] * vk[k + 4];
+          for (int k = 0; k < 8; ++k) vk[k] = vv[k];
+          const double gfx = g[0] * vk[0] + g[4] * vk[1];
+          const double gfy = g[9] * vk[2] + g[13] * vk[3];
+          const double gmy = g[19] * vk[4] + g[23] * vk[5];
+          double gz0 = 0.0, gz1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            gz0 += g[4 * k + 2] * vk[k];
+            gz1 += g[4 * (k + 4) + 2] * vk[k + 4];
+          }
+          rv[0] = -RXu[b + foot_colj(f, 0)] - gfx;
+          rv[1] = -RXu[b + foot_colj(f, 1)] - gfy;
+          rv[2] = -RXu[b + foot_colj(f, 2)] - (gz0 + gz1);
+          rv[3] = -RXu[b + foot_colj(f, 3)] - gmy;
         }
-        rv[0] = -RXu[b + foot_colj(f, 0)] - gfx;
-        rv[1] = -RXu[b + foot_colj(f, 1)] - gfy;
-        rv[2] = -RXu[b + foot_colj(f, 2)] - (gz0 + gz1);
-        rv[3] = -RXu[b + foot_colj(f, 3)] - gmy;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
@@ -850,6 +944,10 @@ struct RegCtx {
     PROF_ADD(4);
   }
 
+  // kRefine: the solve of the refinement step -- dx becomes the saved dx + the correction before
+  // dz and ds are formed from it (with the combined solve's VV, r_s); dy stays the correction (the
+  // update adds the saved dy)
+  template <bool kRefine = false>
   SRBD_PHASE_ATTR __device__ void solve_finish() {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
@@ -862,7 +960,7 @@ struct RegCtx {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         if (k < N) aty += mcol(Mc, j, QV + 12 * k);
-        TV[c] = TV[c] - aty * IX[j];
+        TV[c] = kRefine ? xsg[c] + (TV[c] - aty * IX[j]) : TV[c] - aty * IX[j];
       }
     }
     if (lane < 3 * N) {
@@ -881,16 +979,24 @@ struct RegCtx {
           double t = 0.0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
-          TV[b + foot_colj(f, a)] -= t;
+          const int o = b + foot_colj(f, a);
+          TV[o] = kRefine ? xsg[o] + (TV[o] - t) : TV[o] - t;
         }
       } else {
         const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
         const double a6 = ncol<false>(Nd, 6, yi, 0), a9 = ncol<false>(Nd, 9, yi, 0);
         const double a8 = ncol<false>(Nd, 8, yi, 0), a11 = ncol<false>(Nd, 11, yi, 0);
-        TV[b + 6] -= SG[0] * a6;
-        TV[b + 9] -= SG[2] * a9;
-        TV[b + 8] -= SG[1] * a8;
-        TV[b + 11] -= SG[3] * a11;
+        if constexpr (kRefine) {  // the saved dx written by another lane, several barriers ago
+          TV[b + 6] = xsg[b + 6] + (TV[b + 6] - SG[0] * a6);
+          TV[b + 9] = xsg[b + 9] + (TV[b + 9] - SG[2] * a9);
+          TV[b + 8] = xsg[b + 8] + (TV[b + 8] - SG[1] * a8);
+          TV[b + 11] = xsg[b + 11] + (TV[b + 11] - SG[3] * a11);
+        } else {
+          TV[b + 6] -= SG[0] * a6;
+          TV[b + 9] -= SG[2] * a9;
+          TV[b + 8] -= SG[1] * a8;
+          TV[b + 11] -= SG[3] * a11;
+        }
         const double rho6 = -RXu[12 * i + 6] - a6, rho9 = -RXu[12 * i + 9] - a9;
         DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) * SG[8];
         DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) * SG[9];
@@ -948,14 +1054,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= (kFused ? fa.batch : args.batch)) return;
-#ifdef SRBD_HWID_DUMP  // diagnostic builds only: residual slots get HW_ID, XCC_ID, start / end time
-  const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
   const int lane = threadIdx.x;
   constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
   RegCtx<N> C;
   C.L = smem;
   C.lane = lane;
+  C.xsg = (kFused ? fa.out[0] : solver_out(args, 0)) + (size_t)env * nz;
+  C.ysg = (kFused ? fa.out[3] : solver_out(args, 3)) + (size_t)env * p;
   double *Mc = smem + Lo::Mc, *Cc = smem + Lo::Cc, *Nd = smem + Lo::Nd, *Gf = smem + Lo::Gf,
          *K0 = smem + Lo::K0, *K1 = smem + Lo::K1, *Pd = smem + Lo::Pd, *IX = smem + Lo::IX,
          *Hu = smem + Lo::Hu, *SG = smem + Lo::SG;
@@ -1158,24 +1263,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   const double* RXu = smem + Lo::RXu;
   PROF_MARK_CTX(C);
   const int n_iter = kFused ? fa.n_iter : args.n_iter;
-#ifdef SRBD_CHAIN_PRIO  // A/B experiment: progress halves (2 / 0) and +1 inside the block chains
-  auto setp = [](int l) {
-    if (l >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (l == 2) __builtin_amdgcn_s_setprio(2);
-    else if (l == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-  };
-#endif
   for (int it = 0; it < n_iter; ++it) {
-#ifdef SRBD_CHAIN_PRIO
-    const int plvl = (2 * it < n_iter) ? 2 : 0;
-    setp(plvl);
-#define SRBD_CHAIN_UP() setp(plvl + 1)
-#define SRBD_CHAIN_DOWN() setp(plvl)
-#else
-#define SRBD_CHAIN_UP()
-#define SRBD_CHAIN_DOWN()
-#endif
     if constexpr (TPB == 64 && SRBD_PROGRESS_PRIO) {
       // Wave priority falls with this QP's progress (3 over the first quarter of the iterations, 0
       // over the last): of the two waves sharing a SIMD the one further behind issues first, so
@@ -1187,29 +1275,32 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
-#ifdef SRBD_REPEAT_PHASE  // diagnostic builds only (scripts/phase_ablation.py): run one idempotent
-                          // phase twice so the timing difference is its marginal cost
-    if (SRBD_REPEAT_PHASE == 1) (void)C.residuals();
-#endif
     const double mu = C.residuals();
+    int ul = C.fresh_lane();
+    if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)
+      double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+      for (int t = 0; t < Lo::SX; ++t)
+        if (ul + TPB * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + TPB * t] * RXu[ul + TPB * t];
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (ul + TPB * t < m) b += C.rs[t] * C.rs[t];
+#pragma unroll
+      for (int t = 0; t < Lo::SE; ++t)
+        if (RegCtx<N>::erow(ul, t).valid) c += C.re[t] * C.re[t];
+      res0 = sqrt(C.block_sum(a));
+      res1 = sqrt(C.block_sum(b));
+      res2 = sqrt(C.block_sum(c));
+    }
     PROF_ADD_CTX(C, 0);
-#ifdef SRBD_REPEAT_PHASE
-    if (SRBD_REPEAT_PHASE == 2) C.factor();
-    if (SRBD_REPEAT_PHASE == 4) C.factor_build();
-#endif
     C.factor_build();
-    C.solve_rhs(0, 0.0);
-    SRBD_CHAIN_UP();
+    C.template solve_rhs<0>(0.0);
     C.template factor_chain<true>();  // + the affine forward elimination
-#ifdef SRBD_REPEAT_PHASE
-    if (SRBD_REPEAT_PHASE == 3) C.solve(0, 0.0);
-#endif
     C.template solve_chain<true>();
-    SRBD_CHAIN_DOWN();
     C.solve_finish();
     const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
     double sza = 0.0;
-    int ul = C.fresh_lane();
+    ul = C.fresh_lane();
 #pragma unroll
     for (int t = 0; t < SI; ++t)
       if (ul + TPB * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
@@ -1218,15 +1309,11 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
     __syncthreads();
     PROF_ADD_CTX(C, 5);
-#ifdef SRBD_CHAIN_PRIO
-    C.solve_rhs(1, sigma * mu * 1.0);  // C.solve(1, ...) with its chain phase bracketed
-    SRBD_CHAIN_UP();
-    C.template solve_chain<false>();
-    SRBD_CHAIN_DOWN();
-    C.solve_finish();
-#else
-    C.solve(1, sigma * mu * 1.0);  // (spelling the three phases out here costs N = 20 58 more spills)
-#endif
+    C.template solve<1>(sigma * mu * 1.0);  // (spelling the phases out here costs N = 20 spills)
+    // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
+    // K = 10 / 20 parity where no refinement has it (profiles/r02/refinement_parity.txt)
+    C.refine_rhs();
+    C.template solve<2>(0.0);
     const double apc = C.step_length(C.s, C.ds), adc = C.step_length(C.z, C.dz);
     __syncthreads();
     double szn = 0.0;
@@ -1244,28 +1331,15 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         szn += sn * zn;
       }
     }
-    for (int e = ul; e < p; e += TPB) Y[e] = Y[e] + adc * (e < nx ? QV[e] : DYm[e - nx]);
-    mu_new = C.block_sum(szn) / m;
-    if (it == n_iter - 1) {
-      double a = 0.0, b = 0.0, c = 0.0;
-#pragma unroll
-      for (int t = 0; t < Lo::SX; ++t)
-        if (ul + TPB * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + TPB * t] * RXu[ul + TPB * t];
-#pragma unroll
-      for (int t = 0; t < SI; ++t)
-        if (ul + TPB * t < m) b += C.rs[t] * C.rs[t];
-#pragma unroll
-      for (int t = 0; t < Lo::SE; ++t)
-        if (RegCtx<N>::erow(ul, t).valid) c += C.re[t] * C.re[t];
-      res0 = sqrt(C.block_sum(a));
-      res1 = sqrt(C.block_sum(b));
-      res2 = sqrt(C.block_sum(c));
+    // dy = the saved dy (refine_rhs, same lane) + the refinement's correction
+    for (int e = ul; e < p; e += TPB) {
+      const double dye = e < nx ? QV[e] : DYm[e - nx];
+      Y[e] = Y[e] + adc * (C.ysg[e] + dye);
     }
+    mu_new = C.block_sum(szn) / m;
     __syncthreads();
     PROF_ADD_CTX(C, 5);
   }
-#undef SRBD_CHAIN_UP
-#undef SRBD_CHAIN_DOWN
   PROF_FLUSH(C);
   auto outp = [&](int k) { return kFused ? fa.out[k] : solver_out(args, k); };
   double* xo = outp(0) + (size_t)env * nz;
@@ -1290,12 +1364,6 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     ro[2] = res2;
     ro[3] = mu_new;
     mo[0] = mu_new;
-#ifdef SRBD_HWID_DUMP
-    ro[0] = (double)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
-    ro[1] = (double)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
-    ro[2] = (double)dbg_t0;
-    ro[3] = (double)__builtin_amdgcn_s_memrealtime();
-#endif
   }
 }
 

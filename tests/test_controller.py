@@ -252,14 +252,9 @@ def test_dense_scatter_matches_layout(which):
 def test_controller_step_matches_oracle_pipeline(K):
     """prepare -> fused former + K-iteration PDIPM -> wrench against the oracle pipeline.
 
-    K = 20 is the controller default. A truncated interior-point run is path-sensitive on a few
-    near-degenerate envs of this batch (a step-length ratio decided by round-off): their mid-path
-    iterates differ between two correct elimination orders while the converged solutions agree.
-    Measured on MI355X (scripts/diag_path_sensitivity.py), worst env relative wrench error for two kernel builds
-    that differ only in rounding: K = 10 1.0e-7 / 1.0e-7, K = 15 3.8e-4 / 1.8e-4, K = 20 5.1e-6 /
-    1.3e-4, K = 30 1.4e-8 / 2.2e-7; the oracle itself moves <= 1.5e-10 under 1-ulp input noise. So
-    K = 20 asserts bulk agreement (median) plus a loose bound on the path-sensitive envs, and K = 30
-    (converged) asserts every env to 1e-6.
+    K = 20 is the controller default (the reference's 4 x 5 schedule). Every env must meet
+    north_star's 1e-4 relative wrench error at K = 20 and 1e-6 at K = 30 (converged). The wrench is
+    FP32, so errors are relative to max(|wrench|, 1 N).
     """
     from oracle import oracle
     N, B = 10, 128
@@ -274,12 +269,7 @@ def test_controller_step_matches_oracle_pipeline(K):
     w = wrench.cpu().numpy()
     assert w.shape == (B, 2, 6) and w.dtype == np.float32 and cost.shape == (B,)
     err = np.abs(w - ref).max(axis=(1, 2)) / np.maximum(np.abs(ref).max(axis=(1, 2)), 1.0)
-    assert np.median(err) <= 1e-6, np.median(err)
-    if K >= 30:
-        assert err.max() <= 1e-6, err.max()
-    else:
-        assert np.mean(err > 1e-5) <= 0.05, np.sort(err)[-8:]  # a few path-sensitive envs at most
-        assert err.max() <= 1e-3, err.max()
+    assert err.max() <= (1e-6 if K >= 30 else 1e-4), np.sort(err)[-8:]
 
 
 @pytest.mark.gpu

@@ -39,15 +39,20 @@ def test_former_matches_oracle(N, random_gait):
         assert err <= 1e-12, f"output {k} rel err {err:.3e}"
 
 
-# (K, tolerance on x/s/z/y, worst env of 64). The GPU solves the same Newton systems by a
-# different exact elimination (twisted block-tridiagonal dual Schur complement with explicit
-# 12x12 inverses) than the oracle's sparse LDL of the full KKT; round-off differences are ~1e-8
-# per env (median) and reach ~1e-7 in the worst env after the first, longest step (the step length
-# is a min over ratios), then grow as the barrier closes and degenerate swing-leg duals become
-# ill-determined (worst z ~2e-4 at K=20 with medians ~1e-8). Measured in profiles/r01/. The
-# first-stage input u0 -- what the controller applies -- stays <= 1e-6; BASELINE's bar is 1e-4.
-SOLVER_CASES = [(1, 1e-6), (5, 1e-6), (10, 1e-5), (20, 1e-3)]
-U0_TOL = 5e-6
+# (K, tolerance on x/s/z/y, worst env of 64; norm-wise relative per env). The GPU solves the same
+# Newton systems by a different exact elimination (twisted block-tridiagonal dual Schur complement
+# with explicit 12x12 inverses, plus one step of iterative refinement on the full KKT per iteration)
+# than the oracle's sparse LDL^T. Two exact FP64 eliminations of the same KKT do not agree better
+# than the IPM's own sensitivity allows: the oracle vs the independent dense-LU restatement
+# (oracle/pdipm_dense.py) differ by up to 1.4e-12 (K = 1), 7e-12 (K = 5), 1.2e-8 (K = 10) and
+# 4.2e-7 (K = 20) on these workloads (N = 20, seed 100, worst of 64 envs;
+# profiles/r02/refinement_parity.txt). The GPU sits at that floor: worst 2.9e-12 / 8.1e-11 /
+# 2.8e-8 / 9.4e-7. The K = 10 and 20 tolerances are set a few times above the measured floor;
+# BASELINE's bar is 1e-4.
+SOLVER_CASES = [(1, 1e-10), (5, 1e-9), (10, 1e-7), (20, 1e-5)]
+# first-stage input u0 at K = 10 (what the controller applies), relative to max |u0| of the env:
+# worst measured 1.3e-7 (N = 20, 509 randomized-gait envs, test_ragged_batches)
+U0_TOL = 1e-6
 
 
 @pytest.mark.parametrize("N", [10, 20])
@@ -86,7 +91,7 @@ def test_runtime_horizon_solver_matches_oracle(N):
     for k in range(4):
         o = out[k].cpu().numpy()
         assert np.all(np.isfinite(o))
-        assert rel_err_rows(o, ref[k]).max() <= 1e-6, (N, k)
+        assert rel_err_rows(o, ref[k]).max() <= dict(SOLVER_CASES)[K], (N, k)
 
 
 def test_cold_start_matches_explicit_init():
@@ -111,8 +116,7 @@ def test_mpc_solve_end_to_end():
     torch.cuda.synchronize()
     x = out[0].cpu().numpy()
     u_gpu, u_ref = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
-    # the K = 10 tolerances of the solver tests (SOLVER_CASES, U0_TOL): the worst of
-    # 256 envs sits at ~1e-6, the round-off spread of two valid elimination orders of the same KKT
+    # the K = 10 tolerances of the solver tests (SOLVER_CASES, U0_TOL)
     assert rel_err_rows(u_gpu, u_ref).max() <= U0_TOL
     assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
 
@@ -162,7 +166,7 @@ def test_fast_and_general_kernels_agree(N, K):
     with _native.solver_path("general"):
         gen = solver.pdipm(qp, it, N, K)
     torch.cuda.synchronize()
-    tol = 1e-5 if K <= 10 else 2e-4
+    tol = dict(SOLVER_CASES)[K]
     for k in range(4):
         e = rel_err_rows(fast[k].cpu().numpy(), gen[k].cpu().numpy())
         assert e.max() <= tol, (k, e.max())
@@ -184,7 +188,7 @@ def test_mixed_batch_routes_non_invariant_qps_to_the_general_kernel():
     for k in range(4):
         e = rel_err_rows(out[k].cpu().numpy(), ref[k])
         assert np.all(np.isfinite(out[k].cpu().numpy()))
-        assert e.max() <= 1e-6, (k, e.max())
+        assert e.max() <= dict(SOLVER_CASES)[K], (k, e.max())
     assert np.all(np.isfinite(out[5].cpu().numpy()))  # no fallback sentinel left behind
 
 
@@ -211,7 +215,9 @@ def test_cusadi_dropin_random_inputs(fn_kind):
     ref = oracle.qp_former(N, np_in) if fn_kind == "qp_former" else oracle.pdipm(N, 5, np_in)
     for k in range(fn.n_out()):
         err = rel_err_rows(cf.outputs_sparse[k].cpu().numpy(), ref[k])
-        assert err.max() <= (1e-12 if fn_kind == "qp_former" else 1e-6), (k, err.max())
+        # uniformly random QP data (no stage structure, uncontrolled conditioning; the general
+        # kernel): worst z 2.8e-9 of 256 envs at K = 5 measured, vs 7e-12 on SRBD QPs
+        assert err.max() <= (1e-12 if fn_kind == "qp_former" else 1e-8), (k, err.max())
     dense = cf.getDenseOutput(2 if fn_kind == "qp_former" else 0).cpu().numpy()
     if fn_kind == "qp_former":
         assert np.allclose(dense, layout.to_dense(ref[2], *layout.ccs_A(N), (14 * N, 24 * N)), atol=1e-12)
@@ -301,3 +307,29 @@ def test_empty_batch_is_a_no_op():
     former = solver.qp_former(empty, N)
     torch.cuda.synchronize()
     assert all(t.shape[0] == 0 for t in out) and all(t.shape[0] == 0 for t in former)
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_golden_fixtures_on_the_hip_path(N):
+    """The committed fixtures (tests/golden/srbd_oracle_N{N}.npz: the reference's two demo points
+    srbd_constraints.py:244-282 and generate_solver_function.py:19-58, two standing and two
+    randomized-gait robots, with the oracle's outputs stored at generation time) through the HIP
+    path: the former bit-level, the cold-started solver and the fused step at every stored K."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"srbd_oracle_N{N}.npz"))
+    inputs = [g[f"in{k}"] for k in range(17)]
+    former = solver.qp_former(_cuda(inputs), N)
+    torch.cuda.synchronize()
+    for name, o in zip("H f A b G d".split(), former):
+        assert rel_err(o.cpu().numpy(), g[name]) <= 1e-12, name
+    qp = _cuda([g["H"], g["G"], g["A"], g["f"], g["d"], g["b"]])
+    for K, tol in SOLVER_CASES:
+        cold = [t.clone() for t in solver.pdipm(qp, None, N, K, y0=1.0)]
+        fused = solver.mpc_solve(_cuda(inputs), N, K, y0=1.0)
+        torch.cuda.synchronize()
+        for k, name in enumerate(["x", "s", "z", "y"]):
+            ref = g[f"K{K}_{name}"]
+            for out in (cold, fused):
+                e = rel_err_rows(out[k].cpu().numpy(), ref)
+                assert e.max() <= tol, (K, name, e.max())
+        np.testing.assert_allclose(fused[5].cpu().numpy(), g[f"K{K}_mu"], rtol=1e-6)
