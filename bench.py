@@ -77,9 +77,10 @@ def solver_kernel_name(N: int) -> str:
 
 
 def load_pmc(N: int, B: int, K: int):
-    """HBM bytes per solver launch from the committed rocprofv3 --pmc summary of this kernel."""
+    """HBM bytes per solver launch from the committed rocprofv3 --pmc summary of this kernel (the
+    latest round's profiles/ first)."""
     name = solver_kernel_name(N)
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -94,7 +95,7 @@ def load_sq(N: int, B: int, K: int):
     """VALU / LDS busy shares of the bench kernel from the committed rocprofv3 SQ-counter summary
     (scripts/gpu_sq_counters.sh + scripts/sq_summary.py --json)."""
     name = solver_kernel_name(N)
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_counters_*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_counters_*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):

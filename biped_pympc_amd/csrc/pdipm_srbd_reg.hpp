@@ -325,10 +325,6 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
-  // this QP's output rows of x and y: while the refinement solve runs they hold the first solve's
-  // dx and dy (the LDS has no room for a second direction; each element is written and re-read by
-  // the same lane, and the final iterate overwrites both rows at the end)
-  double *xsg, *ysg;
   PROF_DECL
 
   __device__ double* at(int off) const { return L + off; }
@@ -493,7 +489,7 @@ struct RegCtx {
           else a[8] += lam * go * gz;            // (my, fz)
         }
       }
-      sweep_inverse<4, true>(a);
+      sweep_inverse<4>(a);  // IEEE pivots: Phi_f reaches cond ~1e7 as the barrier sharpens
 #pragma unroll
       for (int e = 0; e < 10; ++e) {
         ph[e] = a[e];
@@ -684,9 +680,7 @@ struct RegCtx {
   }
 
   // ------------------------------------------------------------------------ solve ----
-  // kMode 0: affine rhs r2 = -(S^-1 (s o z)); 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu);
-  // 2: refinement -- the right-hand side is the residual of KKT rows 1 and 4 left in r_x / r_e by
-  // refine_rhs(), rows 2 and 3 have none (VV keeps the combined solve's D^-1 (r2 - W r3)).
+  // kMode 0: affine rhs r2 = -(S^-1 (s o z)); 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu).
   // One solve = solve_rhs (t = Phi^-1 r~ and the dual right-hand side g, in QV) -> solve_chain
   // (the twisted block forward elimination and back substitution: dy in QV) -> solve_finish (dx,
   // dz, ds). The affine solve's forward elimination runs inside factor_chain<true> instead, with
@@ -695,95 +689,92 @@ struct RegCtx {
   __device__ void solve(double smu) {
     solve_rhs<kMode>(smu);
     solve_chain<false>();
-    solve_finish<kMode == 2>();
+    solve_finish<false>();
   }
 
-  // One step of iterative refinement of the combined direction d = (dx, ds, dz, dy). The dual
-  // Schur elimination applies explicit inverses of the 12x12 blocks, whose error is not
-  // backward-stable: along the stiff directions of S (the yaw-moment columns enter S_ii with
-  // 1/(R + beta) = 1e4) dy is off by ~eps cond |dy|, and dx_u = Phi_u^-1 (r - N^T dy) multiplies
-  // that by 1e4 (profiles/r02/refinement_parity.txt: 1e-7 relative in x after one iteration against
-  // the oracle's sparse LDL^T, 1e-12 after this step). The residual of the full KKT of
-  // sparse_pdipm_solver.py:412-439 for d is zero in rows 2 and 3 by construction (ds, dz come from
-  // them), so only rows 1 and 4 are formed:
-  //   e1 = -r_x - (H + beta I) dx - G^T dz - A^T dy,   e4 = -r_e - A dx + delta dy,
-  // left as r_x <- -e1, r_e <- -e4 for solve<2>, whose result is added to the saved d.
-  SRBD_PHASE_ATTR __device__ void refine_rhs() {
-    const int lane = fresh_lane();
-    const double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm), *Mc = at(Lo::Mc),
-                 *Nd = at(Lo::Nd), *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
-    double *Zd = at(Lo::Z), *RXu = at(Lo::RXu), *REm = at(Lo::REm);
-#pragma unroll
-    for (int t = 0; t < SI; ++t) {  // dz to LDS for G^T dz (Z's z mirror is dead until the update)
-      const int q = lane + TPB * t;
-      if (q < m) Zd[q] = dz[t];
-    }
-#pragma unroll
-    for (int t = 0; t < (nz + TPB - 1) / TPB; ++t) {  // save dx, dy (owner lanes, see xsg)
-      const int e = lane + TPB * t;
-      if (e < nz) xsg[e] = TV[e];
-      if (e < p) ysg[e] = e < nx ? QV[e] : DYm[e - nx];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < SX; ++t) {  // x columns: (H_x + beta) dx + r_x + P dy_{k-1} + M^T dy_k
-      const int c = lane + TPB * t;
-      if (c < nx) {
-        const int k = c / 12 + 1, j = c % 12;
-        const double v = (Hu[12 + j] + kBeta) * TV[c] + rxx[t];
-        double ay = Pd[j] * QV[12 * (k - 1) + j];
-        if (k < N) ay += mcol(Mc, j, QV + 12 * k);
-        rxx[t] = v + ay;
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < SX; ++t) {  // u columns: (H_u + beta) du + r_x + G^T dz + N^T dy + e-rows
-      const int c = lane + TPB * t;
-      if (c < nx) {
-        const int i = c / 12, j = c % 12;
-        const double v = (Hu[j] + kBeta) * TV[nx + c] + RXu[c];
-        double gz = 0.0;
-        const int f = foot_of(j);
-        if (f >= 0) {
-          const int a = foot_pos(j);
-          const double* zf = Zd + 16 * i + 8 * f;
-          const double* g = Gf + 32 * f + a;
-          double g0 = 0.0, g1 = 0.0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            g0 += g[4 * k] * zf[k];
-            g1 += g[4 * (k + 4)] * zf[k + 4];
-          }
-          gz = g0 + g1;
-        }
-        double ay = ncol(Nd, j, QV + 12 * i, j % 3);
-        if (j == 6) ay += SG[6] * DYm[2 * i];
-        if (j == 9) ay += SG[7] * DYm[2 * i + 1];
-        RXu[c] = (v + gz) + ay;
-      }
-    }
-    re_refine<0>(TV, QV, Mc, Pd, Nd);
-    re_refine<1>(TV, QV, Mc, Pd, Nd);
-    {
-      const ERow q = erow(lane, 2);
-      if (q.valid) {
-        const int w = q.r;
-        re[2] = (SG[6 + w] * TV[nx + 12 * q.i + (w ? 9 : 6)] + re[2]) - kDelta * DYm[q.e - nx];
-        REm[q.e - nx] = re[2];
-      }
-    }
-    __syncthreads();
-  }
+  // One step of iterative refinement of the combined direction d = (dx, ds, dz, dy) against the
+  // full KKT of sparse_pdipm_solver.py:412-439. The chains' explicit 12x12 block inverses are not
+  // backward-stable along the stiff directions of S (the yaw-moment columns enter S_ii with
+  // 1/(R + beta) = 1e4, and the packed store keeps one of the two rounding-different halves of each
+  // symmetric inverse), so dy is off by ~eps cond |dy| and dx_u = Phi_u^-1 (r - N^T dy) multiplies
+  // that by 1e4: 1e-7 relative in x after one iteration against the oracle's sparse LDL^T; and as
+  // the barrier sharpens (W = z / s -> 1e8) the reduced foot rows r~ = -r_x - G^T D^-1 (r2 - W r3)
+  // cancel against Phi_f dx_f. Rows 2 and 3 hold by construction (ds, dz are formed from them);
+  // the correction K [cx; cy] = [e1; e4] is taken block Gauss-Seidel, which is the same elimination
+  // (cx = Phi^-1 (e1 - A^T cy), S cy = A Phi^-1 e1 - e4):
+  //   1. dx_f += Phi_f^-1 e1_f on the foot columns, e1 = -r_x - (H + beta) dx - G^T dz - A^T dy
+  //      (the other columns' Phi is diagonal and their row-1 residual is rounding only);
+  //   2. rho = A_dyn dx + r_e - delta dy, KKT row 4's residual = the dual residual g - S dy
+  //      (the x-moment rows are eliminated exactly by their 2x2 blocks);
+  //   3. one more chain solve S c = rho; dy += c, dx -= Phi~^-1 A^T c (solve_finish<true>, which
+  //      leaves row 1 as step 1 made it) and dz, ds re-formed from dx.
+  // This sits at the dense-LU-vs-oracle floor over 512 envs per case at K = 1/10/20 (the full
+  // residual of both rows with a second right-hand-side solve measures the same and costs 6 % more
+  // on the fused step: profiles/r02/refinement_variants.txt). dy is parked in RXu (r_x's u part is
+  // dead once step 1 has read it) while QV carries rho and then c.
   template <int t>
-  __device__ void re_refine(const double* TV, const double* QV, const double* Mc, const double* Pd,
-                            const double* Nd) {  // r_e <- A dx + r_e - delta dy (dynamics rows)
+  __device__ void rho_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV,
+                           double* DYs) {
     const ERow q = erow(fresh_lane(), t);
     if (q.valid) {
       double v = (q.i >= 1) ? mrow(Mc, q.r, TV + 12 * (q.i - 1)) : 0.0;
       v += Pd[q.r] * TV[12 * q.i + q.r];
       v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
-      re[t] = (v + re[t]) - kDelta * QV[q.e];
+      const double dy = QV[q.e];  // read and rewritten by its owner lane only
+      DYs[q.e] = dy;
+      QV[q.e] = (v + re[t]) - kDelta * dy;
     }
+  }
+  SRBD_PHASE_ATTR __device__ void refine_rhs() {
+    const int lane = fresh_lane();
+    const double *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
+    double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z);
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // dz to LDS for G^T dz (Z's z mirror is dead until the update)
+      const int q = lane + TPB * t;
+      if (q < m) Zd[q] = dz[t];
+    }
+    __syncthreads();
+    if (lane < 2 * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
+      const int i = lane >> 1, f = lane & 1, b = 12 * i;
+      const double* zf = Zd + 16 * i + 8 * f;
+      const double* RXu = DYs;
+      const double* g = Gf + 32 * f;  // (G^T dz)_a over column a's structural rows (as solve_rhs)
+      double gt[4];
+      {
+        double zk[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) zk[k] = zf[k];
+        gt[0] = g[0] * zk[0] + g[4] * zk[1];
+        gt[1] = g[9] * zk[2] + g[13] * zk[3];
+        gt[3] = g[19] * zk[4] + g[23] * zk[5];
+        double gz0 = 0.0, gz1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          gz0 += g[4 * k + 2] * zk[k];
+          gz1 += g[4 * (k + 4) + 2] * zk[k + 4];
+        }
+        gt[2] = gz0 + gz1;
+      }
+      double e1[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int j = foot_colj(f, a);
+        const double ay = a < 3 ? ncol(Nd, j, QV + b, a) : ncol<false>(Nd, j, QV + b, 0);
+        e1[a] = ((-RXu[b + j] - (Hu[j] + kBeta) * TV[nx + b + j]) - gt[a]) - ay;
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * e1[q];
+        TV[nx + b + foot_colj(f, a)] += t;
+      }
+    }
+    __syncthreads();
+    rho_slot<0>(TV, Mc, Pd, Nd, QV, DYs);
+    rho_slot<1>(TV, Mc, Pd, Nd, QV, DYs);
+    __syncthreads();
   }
 
   template <int kMode>
@@ -792,16 +783,14 @@ struct RegCtx {
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
                  *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd);
-    if constexpr (kMode != 2) {
 #pragma unroll
-      for (int t = 0; t < SI; ++t) {
-        const int q = lane + TPB * t;
-        if (q < m) {
-          const double si = rcp3(s[t]);
-          double r2 = -(si * (s[t] * z[t]));
-          if (kMode == 1) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
-          VV[q] = di[t] * (r2 + wd[t] * rs[t]);
-        }
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + TPB * t;
+      if (q < m) {
+        const double si = rcp3(s[t]);
+        double r2 = -(si * (s[t] * z[t]));
+        if (kMode == 1) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
+        VV[q] = di[t] * (r2 + wd[t] * rs[t]);
       }
     }
 #pragma unroll
@@ -815,10 +804,7 @@ struct RegCtx {
       if (lane < 2 * N) {
         const int i = lane >> 1, f = lane & 1, b = 12 * i;
         double rv[4];
-        if constexpr (kMode == 2) {
-#pragma unroll
-          for (int a = 0; a < 4; ++a) rv[a] = -RXu[b + foot_colj(f, a)];
-        } else {
+        {
           const double* vv = VV + 16 * i + 8 * f;
           const double* g = Gf + 32 * f;  // (G^T vv)_a over column a's structural rows
           double vk[8];
@@ -944,9 +930,9 @@ struct RegCtx {
     PROF_ADD(4);
   }
 
-  // kRefine: the solve of the refinement step -- dx becomes the saved dx + the correction before
-  // dz and ds are formed from it (with the combined solve's VV, r_s); dy stays the correction (the
-  // update adds the saved dy)
+  // kRefine: the refinement step -- TV holds dx and QV the dual correction c, so the same updates
+  // give dx - Phi~^-1 A^T c; the x-moment duals move by their 2x2 formula's increment, and dz, ds are
+  // re-formed from the refined dx (with the combined solve's VV, r_s)
   template <bool kRefine = false>
   SRBD_PHASE_ATTR __device__ void solve_finish() {
     const int lane = fresh_lane();
@@ -960,7 +946,7 @@ struct RegCtx {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         if (k < N) aty += mcol(Mc, j, QV + 12 * k);
-        TV[c] = kRefine ? xsg[c] + (TV[c] - aty * IX[j]) : TV[c] - aty * IX[j];
+        TV[c] = TV[c] - aty * IX[j];
       }
     }
     if (lane < 3 * N) {
@@ -980,26 +966,24 @@ struct RegCtx {
 #pragma unroll
           for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
           const int o = b + foot_colj(f, a);
-          TV[o] = kRefine ? xsg[o] + (TV[o] - t) : TV[o] - t;
+          TV[o] = TV[o] - t;
         }
       } else {
-        const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
+        const double r4a = kRefine ? 0.0 : -REm[2 * i], r4b = kRefine ? 0.0 : -REm[2 * i + 1];
         const double a6 = ncol<false>(Nd, 6, yi, 0), a9 = ncol<false>(Nd, 9, yi, 0);
         const double a8 = ncol<false>(Nd, 8, yi, 0), a11 = ncol<false>(Nd, 11, yi, 0);
-        if constexpr (kRefine) {  // the saved dx written by another lane, several barriers ago
-          TV[b + 6] = xsg[b + 6] + (TV[b + 6] - SG[0] * a6);
-          TV[b + 9] = xsg[b + 9] + (TV[b + 9] - SG[2] * a9);
-          TV[b + 8] = xsg[b + 8] + (TV[b + 8] - SG[1] * a8);
-          TV[b + 11] = xsg[b + 11] + (TV[b + 11] - SG[3] * a11);
+        TV[b + 6] -= SG[0] * a6;
+        TV[b + 9] -= SG[2] * a9;
+        TV[b + 8] -= SG[1] * a8;
+        TV[b + 11] -= SG[3] * a11;
+        if constexpr (kRefine) {  // dy_E = (e rho - phi r4) / (phi delta + e^2), rho = -r_x - a
+          DYm[2 * i] -= (SG[6] * a6) * SG[8];
+          DYm[2 * i + 1] -= (SG[7] * a9) * SG[9];
         } else {
-          TV[b + 6] -= SG[0] * a6;
-          TV[b + 9] -= SG[2] * a9;
-          TV[b + 8] -= SG[1] * a8;
-          TV[b + 11] -= SG[3] * a11;
+          const double rho6 = -RXu[12 * i + 6] - a6, rho9 = -RXu[12 * i + 9] - a9;
+          DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) * SG[8];
+          DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) * SG[9];
         }
-        const double rho6 = -RXu[12 * i + 6] - a6, rho9 = -RXu[12 * i + 9] - a9;
-        DYm[2 * i] = (SG[6] * rho6 - SG[4] * r4a) * SG[8];
-        DYm[2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) * SG[9];
       }
     }
     __syncthreads();
@@ -1059,8 +1043,6 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   RegCtx<N> C;
   C.L = smem;
   C.lane = lane;
-  C.xsg = (kFused ? fa.out[0] : solver_out(args, 0)) + (size_t)env * nz;
-  C.ysg = (kFused ? fa.out[3] : solver_out(args, 3)) + (size_t)env * p;
   double *Mc = smem + Lo::Mc, *Cc = smem + Lo::Cc, *Nd = smem + Lo::Nd, *Gf = smem + Lo::Gf,
          *K0 = smem + Lo::K0, *K1 = smem + Lo::K1, *Pd = smem + Lo::Pd, *IX = smem + Lo::IX,
          *Hu = smem + Lo::Hu, *SG = smem + Lo::SG;
@@ -1313,7 +1295,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
     // K = 10 / 20 parity where no refinement has it (profiles/r02/refinement_parity.txt)
     C.refine_rhs();
-    C.template solve<2>(0.0);
+    C.template solve_chain<false>();
+    C.template solve_finish<true>();
     const double apc = C.step_length(C.s, C.ds), adc = C.step_length(C.z, C.dz);
     __syncthreads();
     double szn = 0.0;
@@ -1331,10 +1314,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         szn += sn * zn;
       }
     }
-    // dy = the saved dy (refine_rhs, same lane) + the refinement's correction
+    // dy = the combined solve's dy (parked in RXu by refine_rhs) + the refinement's correction
     for (int e = ul; e < p; e += TPB) {
-      const double dye = e < nx ? QV[e] : DYm[e - nx];
-      Y[e] = Y[e] + adc * (C.ysg[e] + dye);
+      const double dye = e < nx ? RXu[e] + QV[e] : DYm[e - nx];
+      Y[e] = Y[e] + adc * dye;
     }
     mu_new = C.block_sum(szn) / m;
     __syncthreads();

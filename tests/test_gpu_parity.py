@@ -6,6 +6,8 @@ of CasADi (absent here; see oracle/srbd_oracle.c). Tolerances are norm-wise rela
 (max |gpu - oracle| / max |oracle| per output); the bar from BASELINE.json is 1e-4 on the QP
 solution, the former is checked at 1e-12.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -16,6 +18,7 @@ from oracle import oracle
 from tests._util import rel_err, rel_err_rows
 
 pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -264,7 +267,12 @@ def test_ragged_batches(N, B):
     assert np.all(np.isfinite(x))
     u_gpu, u_ref = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
     assert rel_err_rows(u_gpu, u_ref).max() <= U0_TOL
-    assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
+    # per env: the K = 10 tolerance, or 4x the spread between the two CPU restatements (sparse
+    # LDL^T oracle vs dense LU, tests/golden/make_dense_floor.py) where that FP64 floor is higher
+    # (one env of the N = 20, 509-env workload sits at 1.1e-7 between them)
+    floor = np.load(os.path.join(GOLDEN, "dense_floor_ragged.npz"))[f"N{N}_B{B}"]
+    err = rel_err_rows(x, ref[0])
+    assert np.all(err <= np.maximum(dict(SOLVER_CASES)[K], 4.0 * floor)), (err.max(), floor[err.argmax()])
 
 
 @pytest.mark.parametrize("N,B,random_gait", [(10, 4096, False), (20, 4096, False), (10, 8192, False),
@@ -316,7 +324,7 @@ def test_golden_fixtures_on_the_hip_path(N):
     randomized-gait robots, with the oracle's outputs stored at generation time) through the HIP
     path: the former bit-level, the cold-started solver and the fused step at every stored K."""
     import os
-    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"srbd_oracle_N{N}.npz"))
+    g = np.load(os.path.join(GOLDEN, f"srbd_oracle_N{N}.npz"))
     inputs = [g[f"in{k}"] for k in range(17)]
     former = solver.qp_former(_cuda(inputs), N)
     torch.cuda.synchronize()
