@@ -55,12 +55,16 @@ def parse():
     p.add_argument("--kernel-reps", type=int, default=10)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
     return p.parse_args()
 
 
-def event_time_ms(fn, reps: int) -> float:
-    """Average duration of fn() on torch's current stream (where the kernels are launched)."""
+def event_time_ms(fn, reps: int, warm: int = 2) -> float:
+    """Average duration of fn() on torch's current stream (where the kernels are launched), after
+    `warm` untimed calls (first-launch attribute setup, clock ramp)."""
     s = torch.cuda.current_stream()
+    for _ in range(warm):
+        fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
@@ -104,6 +108,17 @@ def load_sq(N: int, B: int, K: int):
                 and name in (d.get("kernel") or "") and d.get("utilisation")):
             return dict(d["utilisation"], source=os.path.relpath(path, ROOT))
     return None
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -183,6 +198,27 @@ def main():
     ms_fused = event_time_ms(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), a.kernel_reps)
     fused = N in (10, 20)
     ms_main = ms_fused if fused else ms_pdipm
+    # the whole controller step: input prep + former + PDIPM + wrench in ONE launch
+    # (srbd_mpc_step) vs the same three stages as three launches, on B synthetic robots
+    ctrl = None
+    if N in (10, 20) and not a.no_controller:
+        from biped_pympc_amd.utils.synthetic import make_controller
+        c = make_controller(B, N, seed=77 + rank, device=dev, n_iter=K)
+
+        def ab(cc):  # one launch vs three launches, interleaved so clock drift hits both alike
+            ones, threes = [], []
+            for _ in range(3):
+                ones.append(event_time_ms(cc.run, a.kernel_reps))
+                threes.append(event_time_ms(cc.run_three_kernel, a.kernel_reps))
+            return sum(ones) / 3, sum(threes) / 3
+        ms_one, ms_three = ab(c)
+        ctrl = {"one_launch_ms": round(ms_one, 4), "three_kernel_ms": round(ms_three, 4),
+                "robots_per_s": round(B / (ms_one * 1e-3), 1),
+                "bytes_out_per_env": 48, "note": "prep + former + PDIPM + wrench; wrench-only output"}
+        c256 = make_controller(256, N, seed=78 + rank, device=dev, n_iter=K)
+        m1, m3 = ab(c256)
+        ctrl["b256"] = {"one_launch_ms": round(m1, 4), "three_kernel_ms": round(m3, 4)}
+        del c, c256
     ms_gather = None
     if dist is not None:
         u0 = bufs.outputs[0][:, 12 * N:12 * N + 12]
@@ -196,12 +232,12 @@ def main():
         hbm_bytes = (w["bytes_fused"] if fused else w["bytes_pdipm_cold"]) * B
         traffic, traffic_src = load_pmc(N, B, K)
         roofline = {
-            "bound": "mfma", "kernel": solver_kernel_name(N), "achieved": round(achieved, 4),
+            "bound": "fp64-valu", "kernel": solver_kernel_name(N), "achieved": round(achieved, 4),
             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
             "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_main, 4),
-            "note": ("FP64 compute roof (vector == matrix peak on MI355X); kernel runs on the "
-                     "FP64 VALU. Flops = the reference's sparse-LDL KKT work per iteration "
+            "note": ("FP64 compute roof (vector == matrix peak on MI355X); the kernel runs on the "
+                     "FP64 VALU (no MFMA): bound = its issue rate and the 12x12 chains. Flops = the reference's sparse-LDL KKT work per iteration "
                      "(SURVEY 8d) x iterations x QPs per launch. Bytes = former inputs in + "
                      "solution out per QP (fused step)." if fused else
                      "FP64 compute roof; flops as SURVEY 8d; bytes = QP in + solution out."),
@@ -214,9 +250,13 @@ def main():
 
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         from oracle import oracle  # cpu_baseline leg: the oracle as baseline and checker only
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        host_cpus = os.cpu_count() or 1
+        affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host_cpus
+        # OpenMP over envs on this process's CPU share: OMP_NUM_THREADS where the harness sets it
+        # (the GPU box gives one GPU's job 16 CPUs of a larger host), else every CPU it may run on
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
         sample = min(B, 512)
         sub = [x[:sample] for x in wl.inputs]
         oracle.mpc_solve(N, K, [x[:8] for x in sub], nthreads=threads)  # symbolic setup + warm
@@ -226,19 +266,42 @@ def main():
             ref = oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=threads)
             t_cpu += time.perf_counter() - t1
             solves += sample
+        # BASELINE config 1 (B = 1, N = 10, K = 5: the reference's CPU-runnable case) on one core,
+        # and B = 256 at the bench's K on the same CPU share
+        one = [x[:1] for x in wl.inputs]
+        n1, t1s = 0, 0.0
+        while t1s < 1.0:
+            t1 = time.perf_counter()
+            oracle.mpc_solve(N, 5, one, y0=1.0, nthreads=1)
+            t1s += time.perf_counter() - t1
+            n1 += 1
+        sub256 = [x[:256] for x in wl.inputs]
+        t1 = time.perf_counter()
+        oracle.mpc_solve(N, K, sub256, y0=1.0, nthreads=threads)
+        t256 = time.perf_counter() - t1
         cpu = {"value": round(solves / t_cpu, 1), "unit": "solves/s", "cores": threads,
-               "kind": "port",
-               "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs) on the first "
-                          f"{sample} envs of the same workload, {solves // sample} passes, "
-                          f"{t_cpu:.1f} s, N={N}, {K} iterations")}
-        step()
+               "kind": "port", "per_core": round(solves / t_cpu / threads, 1),
+               "host": {"logical_cpus": host_cpus, "affinity_cpus": affinity, "model": _cpu_model()},
+               "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs, {threads} threads) on "
+                          f"the first {sample} envs of the same workload, {solves // sample} passes, "
+                          f"{t_cpu:.1f} s, N={N}, {K} iterations"),
+               "config1_b1_k5": {"ms_per_solve": round(1e3 * t1s / n1, 4), "cores": 1},
+               "b256": {"solves_per_s": round(256 / t256, 1), "cores": threads, "iters": K}}
+        # GPU latency of the same two small configurations (one launch each, resident inputs)
+        g1 = [t[:1].contiguous() for t in inputs]
+        g256 = [t[:256].contiguous() for t in inputs]
+        cpu["config1_b1_k5"]["gpu_ms"] = round(event_time_ms(lambda: solver.mpc_solve(g1, N, 5, 1.0), a.kernel_reps), 4)
+        cpu["b256"]["gpu_ms"] = round(event_time_ms(lambda: solver.mpc_solve(g256, N, K, 1.0), a.kernel_reps), 4)
+        x = solver.mpc_solve([t[:sample].contiguous() for t in inputs], N, K, 1.0)[0]
         torch.cuda.synchronize()
-        x = sh.x_local[:sample].cpu().numpy()
+        x = x.cpu().numpy()
         ug, ur = x[:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]
         du = np.abs(ug - ur)
         parity = {"max_abs_du": float(du.max()),
                   "max_rel_du": float((du.max(axis=1) / np.abs(ur).max(axis=1)).max()),
                   "envs": sample, "vs": "oracle (CPU restatement; CasADi unavailable: parity unpinned)"}
+    if dist is not None:
+        dist.barrier()  # the other ranks wait for rank 0's CPU leg before tearing down
 
     if rank == 0:
         line = {
@@ -260,6 +323,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
+            "controller_step": ctrl,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -49,6 +49,8 @@ def lib() -> ctypes.CDLL:
     L.srbd_pdipm_cold.restype = ctypes.c_int
     L.srbd_pdipm_cold.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P,
                                   ctypes.c_void_p]
+    L.srbd_pdipm_ccs.restype = ctypes.c_int
+    L.srbd_pdipm_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_void_p]
     L.srbd_mpc_solve.restype = ctypes.c_int
     L.srbd_mpc_solve.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
                                  ctypes.c_void_p, P, ctypes.c_void_p]
@@ -67,6 +69,9 @@ def lib() -> ctypes.CDLL:
                                    ctypes.POINTER(ctypes.c_int)]
     L.srbd_prepare_inputs.restype = ctypes.c_int
     L.srbd_prepare_inputs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(MPCPrep), P, ctypes.c_void_p]
+    L.srbd_mpc_step.restype = ctypes.c_int
+    L.srbd_mpc_step.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(MPCPrep),
+                                P, P, _c_dp, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
     L.srbd_u0_wrench.restype = ctypes.c_int
     L.srbd_u0_wrench.argtypes = [ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
     L.srbd_u0_wrench_torque.restype = ctypes.c_int
@@ -105,8 +110,8 @@ def check(rc: int, what: str) -> None:
 class solver_path:
     """Context manager selecting the solver kernels: "auto" (stage-invariant kernels -- the
     register-resident one at N = 10 and 20 -- plus the general fallback), "general" (general kernel only)
-    or "lds" (the LDS-resident stage-invariant kernel at every horizon). Process-wide; for
-    tests/benchmarks."""
+    or "lds" (the LDS-resident stage-invariant kernel at every horizon). For the current HIP device;
+    for tests/benchmarks."""
 
     def __init__(self, path: str):
         self.code = {"auto": 0, "general": 1, "lds": 2}[path]

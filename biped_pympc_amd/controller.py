@@ -6,13 +6,15 @@ Mirrors the reference controller API so a user of ``MPCControllerCusadi`` can sw
   * ``BaseMPCController`` setters and knot-point state (``convex_mpc/base_controller.py:11-266``),
   * ``MPCControllerHIP.run() -> (foot_wrench (B,2,6) float32, cost (B,))`` with the semantics of
     ``MPCControllerCusadi.run`` (``convex_mpc/mpc_controller_cusadi.py:43-205``).
-The whole step runs as three kernels on the caller's current HIP stream with no host
-synchronisation: ``srbd_prepare_inputs`` (knot points, initial state, reference trajectory,
-contact schedule, I_world -- the ~40 small FP32 torch ops of the reference), the fused former +
-PDIPM (cold start, ``cfg.pdipm_iterations`` Newton iterations in one launch; the reference runs
-a former call and 4 solver calls x 5 iterations with host round trips) and ``srbd_u0_wrench``;
-``GraphedMPCStep`` replays the three as one captured HIP graph. Nothing of the step is computed in
-PyTorch; it only owns the buffers.
+At N = 10 and 20 the whole step is ONE kernel launch on the caller's current HIP stream with no
+host synchronisation (``srbd_mpc_step``): the input preparation (knot points, initial state,
+reference trajectory, contact schedule, I_world -- the ~40 small FP32 torch ops of the reference)
+into on-chip memory, the fused former + PDIPM (cold start, ``cfg.pdipm_iterations`` Newton
+iterations; the reference runs a former call and 4 solver calls x 5 iterations with host round
+trips) and the u0 -> wrench (-> stance torque) epilogue; only the (B, 2, 6) wrench leaves the chip
+unless ``cfg.keep_solution``. Other horizons run the same three stages as three kernels
+(``run_three_kernel``, bit-identical at N = 10 / 20). ``GraphedMPCStep`` replays the step as a
+captured HIP graph. Nothing of the step is computed in PyTorch; it only owns the buffers.
 
 ``literal_layout=True`` (default) reproduces the reference GPU caller's flattening quirks
 (row-major R_body read column-major, row-major contact table read column-major, a 13-wide Q read
@@ -54,6 +56,8 @@ class MPCConf:
     pdipm_iterations: int = 20  # the reference GPU caller: 4 calls x 5 iterations (:28, :144)
     y0: float = 1.0             # dual init of the GPU caller (:141)
     literal_layout: bool = True
+    keep_solution: bool = False  # also write the QP solution (x, s, z, y, residuals, mu) to .solution
+    #                              and the 17 prepared former inputs to .former_inputs
 
 
 @dataclass
@@ -116,6 +120,7 @@ class BaseMPCController:
         self.desired_state_data: DesiredStateData | None = None
         self.leg_controller_data = None
         self.first_run = torch.ones(num_envs, device=self.device, dtype=torch.bool)
+        self._version = 0  # bumped by every setter that replaces a tensor (GraphedMPCStep checks it)
         robot = ROBOTS[cfg.robot]
         self.mass, self.mu = robot["mass"], robot["mu"]
         self.I_body = torch.tensor(robot["I_body"], dtype=torch.float32)
@@ -139,9 +144,11 @@ class BaseMPCController:
     # ---- setters (base_controller.py:98-142) ----
     def set_state_estimate_data(self, state_estimate_data: StateEStimatorData) -> None:
         self.state_estimate_data = state_estimate_data
+        self._version += 1
 
     def set_desired_state_data(self, desired_state_data: DesiredStateData) -> None:
         self.desired_state_data = desired_state_data
+        self._version += 1
 
     def set_leg_controller_data(self, leg_controller_data) -> None:
         self.leg_controller_data = leg_controller_data
@@ -150,6 +157,7 @@ class BaseMPCController:
         """Explicit (B, N, 2) contact schedule (what GaitGenerator.mpc_gait returns)."""
         self.contact_table = _f32(contact_table, self.device)
         self._gait = None
+        self._version += 1
 
     def set_gait(self, gait_phase: torch.Tensor, ssp_durations: torch.Tensor, dsp_durations: torch.Tensor) -> None:
         """Device-side contact schedule: the kernel evaluates GaitGenerator.mpc_gait
@@ -157,9 +165,11 @@ class BaseMPCController:
         self._gait = (_f32(gait_phase, self.device),
                       ssp_durations.to(device=self.device, dtype=torch.int32).contiguous(),
                       dsp_durations.to(device=self.device, dtype=torch.int32).contiguous())
+        self._version += 1
 
     def set_mpc_sampling_time(self, dt_mpc: torch.Tensor) -> None:
         self.dt_mpc = dt_mpc
+        self._version += 1
 
     def reset(self, env_ids: torch.Tensor) -> None:
         self.first_run[env_ids] = True
@@ -178,25 +188,31 @@ class MPCControllerHIP(BaseMPCController):
         self.tau = None  # (B, 2, ndof) float32, allocated by run_with_torque
         return self
 
-    def _prep_struct(self, keep: list) -> _native.MPCPrep:
+    def _prep_struct(self, keep: list, strict: bool = False) -> _native.MPCPrep:
+        """The device-pointer struct of one step. strict (graph capture): every tensor must already
+        be float32, contiguous and on the controller's device -- a converted copy would be baked
+        into the graph and never see the caller's in-place updates."""
         st, ds, dev = self.state_estimate_data, self.desired_state_data, self.device
         if st is None or ds is None:
             raise RuntimeError("set_state_estimate_data / set_desired_state_data before run()")
+
+        def f32(t, name):
+            on_dev = t.device.type == dev.type and (dev.index is None or t.device.index == dev.index)
+            if strict and (t.dtype != torch.float32 or not t.is_contiguous() or not on_dev):
+                raise ValueError(f"GraphedMPCStep: {name} must be a contiguous float32 tensor on {dev} "
+                                 f"(got {t.dtype}, contiguous={t.is_contiguous()}, {t.device})")
+            return _f32(t, dev)
 
         def ptr(t):
             keep.append(t)
             return t.data_ptr()
 
         p = _native.MPCPrep()
-        p.root_euler = ptr(_f32(st.root_euler, dev))
-        p.root_position = ptr(_f32(st.root_position, dev))
-        p.root_angular_velocity_w = ptr(_f32(st.root_angular_velocity_w, dev))
-        p.root_velocity_w = ptr(_f32(st.root_velocity_w, dev))
-        p.rotation_body = ptr(_f32(st.rotation_body, dev))
-        p.foot_position = ptr(_f32(st.foot_position, dev))
-        p.desired_velocity_b = ptr(_f32(ds.desired_velocity_b, dev))
-        p.desired_angular_velocity_b = ptr(_f32(ds.desired_angular_velocity_b, dev))
-        p.desired_height = ptr(_f32(ds.desired_height, dev))
+        for name in ("root_euler", "root_position", "root_angular_velocity_w", "root_velocity_w",
+                     "rotation_body", "foot_position"):
+            setattr(p, name, ptr(f32(getattr(st, name), name)))
+        for name in ("desired_velocity_b", "desired_angular_velocity_b", "desired_height"):
+            setattr(p, name, ptr(f32(getattr(ds, name), name)))
         for name in ("world_position_desired", "yaw_desired"):  # updated in place by the kernel
             t = getattr(self, name)
             if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
@@ -209,10 +225,10 @@ class MPCControllerHIP(BaseMPCController):
         if self._gait is not None:
             p.gait_phase, p.ssp_durations, p.dsp_durations = (ptr(t) for t in self._gait)
         else:
-            p.contact_table = ptr(_f32(self.contact_table, dev))
-        p.dt_mpc = ptr(_f32(self.dt_mpc, dev))
-        p.residual_lin_accel = ptr(_f32(self.residual_lin_accel, dev))
-        p.residual_ang_accel = ptr(_f32(self.residual_ang_accel, dev))
+            p.contact_table = ptr(f32(self.contact_table, "contact_table"))
+        p.dt_mpc = ptr(f32(self.dt_mpc, "dt_mpc"))
+        p.residual_lin_accel = ptr(f32(self.residual_lin_accel, "residual_lin_accel"))
+        p.residual_ang_accel = ptr(f32(self.residual_ang_accel, "residual_ang_accel"))
         p.I_body[:] = [float(v) for v in self.I_body.reshape(-1).tolist()]
         p.mass, p.mu = float(self.mass), float(self.mu)
         q = [float(v) for v in torch.as_tensor(self.Q, dtype=torch.float32).reshape(-1).tolist()]
@@ -236,25 +252,47 @@ class MPCControllerHIP(BaseMPCController):
         _native.check(rc, "srbd_prepare_inputs")
         return self.former_inputs
 
+    def _step(self, p: _native.MPCPrep, J: torch.Tensor | None, cb: torch.Tensor | None) -> None:
+        """One srbd_mpc_step launch: prep -> fused former + PDIPM -> wrench (-> torque)."""
+        N, B = self.horizon_length, self.num_envs
+        outs = (_native.ptr_array([t.data_ptr() for t in self.buffers.outputs])
+                if self.cfg.keep_solution else None)
+        fin = (_native.ptr_array([t.data_ptr() for t in self.former_inputs])
+               if self.cfg.keep_solution else None)
+        rc = _native.lib().srbd_mpc_step(
+            N, self.cfg.pdipm_iterations, B, float(self.cfg.y0), ctypes.byref(p), fin, outs,
+            self.foot_wrench.data_ptr(), 0 if J is None else J.shape[3], None if J is None else J.data_ptr(),
+            None if cb is None else cb.data_ptr(), None if J is None else self.tau.data_ptr(),
+            solver._stream_ptr())
+        _native.check(rc, "srbd_mpc_step")
+        self.solution = self.buffers.outputs if self.cfg.keep_solution else None
+
     def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        N = self.horizon_length
+        """MPCControllerCusadi.run (mpc_controller_cusadi.py:43-205): (foot_wrench (B,2,6) f32, cost)."""
+        if self.horizon_length not in (10, 20):
+            return self.run_three_kernel()
+        keep: list = []
+        self._step(self._prep_struct(keep), None, None)
+        return self.foot_wrench, self.cost
+
+    def run_three_kernel(self, J: torch.Tensor | None = None, cb: torch.Tensor | None = None):
+        """The same step as three launches (srbd_prepare_inputs -> srbd_mpc_solve_fused ->
+        srbd_u0_wrench_torque) with the 17 former inputs and the solution in device memory; any
+        horizon. Bit-identical to run() at N = 10 / 20 (tests/test_controller.py)."""
+        N, B = self.horizon_length, self.num_envs
         self.prepare()
         out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
         self.solution = out
         rot = _f32(self.state_estimate_data.rotation_body, self.device)
-        rc = _native.lib().srbd_u0_wrench(N, self.num_envs, out[0].data_ptr(), rot.data_ptr(),
-                                          self.foot_wrench.data_ptr(), solver._stream_ptr())
-        _native.check(rc, "srbd_u0_wrench")
-        return self.foot_wrench, self.cost
+        rc = _native.lib().srbd_u0_wrench_torque(
+            N, B, out[0].data_ptr(), rot.data_ptr(), self.foot_wrench.data_ptr(), 0 if J is None else J.shape[3],
+            None if J is None else J.data_ptr(), None if cb is None else cb.data_ptr(),
+            None if J is None else self.tau.data_ptr(), solver._stream_ptr())
+        _native.check(rc, "srbd_u0_wrench_torque")
+        return (self.foot_wrench, self.cost) if J is None else (self.foot_wrench, self.cost, self.tau)
 
-    def run_with_torque(self, contact_jacobian: torch.Tensor, contact_bool: torch.Tensor
-                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """run() plus the stance feed-forward joint torque the wrench feeds
-        (LegController.update_ff_torque, leg_controller.py:87-95, after
-        BipedController._run_stance_leg_controller, biped_controller.py:144-146), computed in the
-        wrench kernel's epilogue: tau (B,2,ndof) float32 = J[:,l]^T wrench[:,l] on stance legs, 0 on
-        swing legs. contact_jacobian (B,2,6,ndof) float32 (LegControllerData.J), contact_bool (B,2)."""
-        N, B = self.horizon_length, self.num_envs
+    def _torque_args(self, contact_jacobian, contact_bool):
+        B = self.num_envs
         J = _f32(contact_jacobian, self.device)
         cb = _f32(contact_bool, self.device)
         if J.dim() != 4 or J.shape[:3] != (B, 2, 6) or cb.shape != (B, 2):
@@ -262,14 +300,20 @@ class MPCControllerHIP(BaseMPCController):
         ndof = J.shape[3]
         if self.tau is None or self.tau.shape != (B, 2, ndof):
             self.tau = torch.empty((B, 2, ndof), dtype=torch.float32, device=self.device)
-        self.prepare()
-        out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
-        self.solution = out
-        rot = _f32(self.state_estimate_data.rotation_body, self.device)
-        rc = _native.lib().srbd_u0_wrench_torque(N, B, out[0].data_ptr(), rot.data_ptr(), self.foot_wrench.data_ptr(),
-                                                 ndof, J.data_ptr(), cb.data_ptr(), self.tau.data_ptr(),
-                                                 solver._stream_ptr())
-        _native.check(rc, "srbd_u0_wrench_torque")
+        return J, cb
+
+    def run_with_torque(self, contact_jacobian: torch.Tensor, contact_bool: torch.Tensor
+                        ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """run() plus the stance feed-forward joint torque the wrench feeds
+        (LegController.update_ff_torque, leg_controller.py:87-95, after
+        BipedController._run_stance_leg_controller, biped_controller.py:144-146), computed in the
+        step's epilogue: tau (B,2,ndof) float32 = J[:,l]^T wrench[:,l] on stance legs, 0 on swing
+        legs. contact_jacobian (B,2,6,ndof) float32 (LegControllerData.J), contact_bool (B,2)."""
+        J, cb = self._torque_args(contact_jacobian, contact_bool)
+        if self.horizon_length not in (10, 20):
+            return self.run_three_kernel(J, cb)
+        keep: list = []
+        self._step(self._prep_struct(keep), J, cb)
         return self.foot_wrench, self.cost, self.tau
 
 
@@ -278,19 +322,21 @@ MPCControllerCusadi = MPCControllerHIP
 
 
 class GraphedMPCStep:
-    """The controller step captured once as a HIP graph and replayed: prepare -> fused former +
-    solver -> wrench (three kernels) become one graph launch, which matters when the batch is
+    """The controller step captured once as a HIP graph and replayed (one graph launch per step;
+    at N = 10 / 20 the graph holds the single srbd_mpc_step kernel). Worth it when the batch is
     small and launch overhead is a visible share of the step.
 
-    The graph records device pointers, so the state / command tensors handed to the controller must
-    keep their storage: update them in place (``copy_``) between replays. Everything else
-    (controller buffers, knot-point state) already lives in fixed tensors.
+    The graph records device pointers, so the state / command / schedule tensors must be contiguous
+    float32 on the controller's device at capture (checked) and be updated IN PLACE (``copy_``)
+    between replays. A setter that replaces a tensor (set_state_estimate_data, set_contact_table,
+    set_gait, set_mpc_sampling_time, ...) invalidates the graph: the next replay raises.
     """
 
     def __init__(self, controller: MPCControllerHIP, warmup: int = 1):
         self.c = controller
         self._keep: list = []
-        self._prep = self.c._prep_struct(self._keep)  # resolves every input pointer once
+        self._prep = self.c._prep_struct(self._keep, strict=True)  # resolves every input pointer once
+        self._version = controller._version
         saved = [t.clone() for t in (controller.world_position_desired, controller.yaw_desired,
                                      controller.first_run)]
         s = torch.cuda.Stream()
@@ -308,6 +354,9 @@ class GraphedMPCStep:
 
     def _launch(self) -> None:
         c, N = self.c, self.c.horizon_length
+        if N in (10, 20):
+            c._step(self._prep, None, None)
+            return
         L = _native.lib()
         _native.check(L.srbd_prepare_inputs(N, c.num_envs, ctypes.byref(self._prep),
                                             _native.ptr_array([t.data_ptr() for t in c.former_inputs]),
@@ -318,6 +367,9 @@ class GraphedMPCStep:
                                        c.foot_wrench.data_ptr(), solver._stream_ptr()), "srbd_u0_wrench")
 
     def __call__(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.c._version != self._version:
+            raise RuntimeError("GraphedMPCStep: a controller setter replaced a captured tensor since the "
+                               "capture; update tensors in place, or capture a new GraphedMPCStep")
         self.graph.replay()
         return self.c.foot_wrench, self.c.cost
 

@@ -37,7 +37,8 @@ struct SolverArgs {
   int N;
   int n_iter;
   int batch;
-  int init_mode;  // 0: iterate from inputs 6..9; 1: x=0, s=max(h,1), z=1, y=y0 (GPU caller init)
+  int init_mode;  // 0: iterate from inputs 6..9; 1: x=0, s=max(h,1), z=1, y=y0 (GPU caller init);
+                  // 2: x = input 6, s = max(h - G x, 1), z = 1, y = 0 (_ccs init)
   int only_flagged;  // 1: solve only QPs the fast kernel flagged (mu output == kFallbackBits)
   double y0;
 };
@@ -96,6 +97,18 @@ __device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
   }
 #pragma unroll
   for (int e = 0; e < n * (n + 1) / 2; ++e) a[e] = -a[e];
+}
+
+// (G x)_q of inequality row q from the stage's 28 CCS values of G (c_tab.grow / gcol) and the u
+// part xu of x, each product rounded: the reference's G_mat @ x_init (sparse_pdipm_solver.py:31);
+// a row holds at most two nonzeros, so every summation order gives this value.
+__device__ inline double ccs_gx(const double* Gv, int q, const double* xu) {
+#pragma clang fp contract(off)
+  const int i = q / 16, k = q % 16;
+  double acc = 0.0;
+  for (int t = 0; t < 28; ++t)
+    if (c_tab.grow[t] == k) acc += Gv[28 * i + t] * xu[12 * i + c_tab.gcol[t]];
+  return acc;
 }
 
 struct SolverCtx {
@@ -573,13 +586,8 @@ struct SolverCtx {
 };
 
 #ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again
-__global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
+__device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int env = blockIdx.x;
-  if (env >= args.batch) return;
-  if (args.only_flagged &&
-      __double_as_longlong(solver_out(args, 5)[env]) != (long long)kFallbackBits)
-    return;
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;
@@ -609,7 +617,13 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   for (int e = lane; e < nA; e += 64) C.AV[e] = Ag[e];
   for (int e = lane; e < nG; e += 64) C.GV[e] = Gg[e];
   for (int e = lane; e < nz; e += 64) C.HV[e] = Hg[e];
-  if (args.init_mode == 0) {
+  if (args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
+    const double* xg = solver_in(args, 6) + (size_t)env * nz;
+    for (int e = lane; e < nz; e += 64) C.X[e] = xg[e];
+    __syncthreads();
+    for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - ccs_gx(Gg, e, C.X + 12 * N), 1.0); C.Z[e] = 1.0; }
+    for (int e = lane; e < p; e += 64) C.Y[e] = 0.0;
+  } else if (args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;
@@ -687,6 +701,20 @@ __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
     ro[2] = res2;
     ro[3] = mu_new;
     mo[0] = mu_new;
+  }
+}
+
+// One workgroup per QP; as the fallback pass behind the stage-invariant kernels (only_flagged) a
+// bounded grid walks the batch and solves just the QPs they flagged (none for qp_former output).
+__global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
+  if (!args.only_flagged) {
+    if ((int)blockIdx.x < args.batch) pdipm_general(args, blockIdx.x);
+    return;
+  }
+  for (int env = blockIdx.x; env < args.batch; env += gridDim.x) {
+    if (__double_as_longlong(solver_out(args, 5)[env]) != (long long)kFallbackBits) continue;
+    pdipm_general(args, env);
+    __syncthreads();  // the next flagged QP reuses this workgroup's LDS
   }
 }
 #endif  // SRBD_NO_GENERAL_KERNEL

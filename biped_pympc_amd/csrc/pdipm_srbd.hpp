@@ -772,7 +772,13 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
     C.K1[e] = k1;
   }
   // ---- iterate ----
-  if (args.init_mode == 0) {
+  if (args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
+    const double* xg = solver_in(args, 6) + (size_t)env * nz;
+    for (int e = lane; e < nz; e += 64) C.X[e] = xg[e];
+    __syncthreads();
+    for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - ccs_gx(Gg, e, C.X + 12 * N), 1.0); C.Z[e] = 1.0; }
+    for (int e = lane; e < p; e += 64) C.Y[e] = 0.0;
+  } else if (args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;

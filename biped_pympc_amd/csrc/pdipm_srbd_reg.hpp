@@ -18,6 +18,7 @@
 #pragma once
 #include "pdipm_srbd.hpp"
 #include "qp_former.hpp"
+#include "mpc_io.hpp"
 
 #ifndef SRBD_PROGRESS_PRIO
 #define SRBD_PROGRESS_PRIO 1  // progress-ordered wave priority (A/B switch for scripts/variant_bench.py)
@@ -775,6 +776,7 @@ struct RegCtx {
     rho_slot<0>(TV, Mc, Pd, Nd, QV, DYs);
     rho_slot<1>(TV, Mc, Pd, Nd, QV, DYs);
     __syncthreads();
+    PROF_ADD(6);
   }
 
   template <int kMode>
@@ -1020,12 +1022,21 @@ struct RegCtx {
 // Arguments of the fused former + solver kernel (srbd_mpc_solve_fused): the 17 qp_former inputs
 // in, the QP's vectors f, b, d written once (row per env, re-read by the same lanes every Newton
 // iteration; the matrices H, A, G never leave the kernel), the solver outputs out.
+// The controller step (srbd_mpc_step) adds the input preparation in front (prep: the 17 former
+// inputs are computed into LDS instead of read from memory) and the foot wrench / stance torque
+// behind (wrench != null). Every out / vec pointer may be null: that array is not written.
 struct FusedArgs {
   const double* in[17];
-  double* vec[3];  // f (B, 24N), b (B, 14N), d (B, 16N)
-  double* out[6];  // x, s, z, y, residuals(4), mu(1)
+  double* vec[3];  // f (B, 24N), b (B, 14N), d (B, 16N), or null
+  double* out[6];  // x, s, z, y, residuals(4), mu(1), each or null
   int N, n_iter, batch;
   double y0;
+  int ctrl;        // 1: former inputs from prepare_env (prep) instead of in[]
+  PrepArgs prep;
+  float* wrench;   // (B, 2, 6) float32, or null
+  const float *jac, *contact;  // (B, 2, 6, ndof), (B, 2) float32 for tau
+  float* tau;      // (B, 2, ndof) float32, or null
+  int ndof;
 };
 
 // Body shared by the solver kernel (kFused = false: the QP comes from qp_former's CCS outputs and is
@@ -1053,10 +1064,31 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     // ---- the stage blocks from the former inputs (qp_former.hpp's former_model) ----
     FormerLds& F = *reinterpret_cast<FormerLds*>(smem + Lo::TV);  // TV..DYm are free until the solve
     static_assert(sizeof(FormerLds) <= sizeof(double) * (Lo::total - Lo::TV), "former scratch fits");
-    const int in_nnz[17] = {12, 12 * N, 12 * N, 12 * N, 1, 1, 1, 9, 9, 3, 3, 3, 2 * N, 12, 12, 3, 3};
     const double* P[17];
+    if (fa.ctrl) {  // controller step: the inputs are prepared here, into DV (dead until the first factor)
+      static_assert(4 * 12 * N + 2 * N + 44 <= 80 * N, "former inputs fit the DV blocks");
+      double* o[17];
+      int off = 0;
 #pragma unroll
-    for (int i = 0; i < 17; ++i) P[i] = fa.in[i] + (size_t)env * in_nnz[i];
+      for (int i = 0; i < 17; ++i) {
+        o[i] = smem + Lo::DV + off;
+        P[i] = o[i];
+        off += former_in_nnz(i, N);
+      }
+      if (lane < 64) prepare_env(fa.prep, env, lane, o);
+      __syncthreads();
+      if (fa.prep.out[0]) {  // the caller also wants the prepared inputs in memory
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+          const int w = former_in_nnz(i, N);
+          double* g = fa.prep.out[i] + (size_t)env * w;
+          for (int e = lane; e < w; e += TPB) g[e] = o[i][e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 17; ++i) P[i] = fa.in[i] + (size_t)env * former_in_nnz(i, N);
+    }
     former_model(F, P, lane);
     const double mu = P[6][0];
     for (int e = lane; e < 144; e += TPB) {
@@ -1077,33 +1109,44 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     __syncthreads();
     if (lane < 28) Gf[4 * c_tab.grow[lane] + foot_pos(c_tab.gcol[lane])] = former_g(lane, mu);
-    // f, b, d rows, each entry written by the lane that reads it in residuals() / the cold init
-    double* fw = fa.vec[0] + (size_t)env * nz;
-    double* bw = fa.vec[1] + (size_t)env * p;
-    double* dw = fa.vec[2] + (size_t)env * m;
+    // f, b, h straight into the registers of the lanes that use them (load_qp_vectors' mapping);
+    // the rows reach memory only if the caller asked for them
 #pragma unroll
     for (int t = 0; t < Lo::SX; ++t) {
-      const int c = lane + TPB * t;
-      if (c < nx) {
-        fw[c] = former_f(c, N, P[13], P[14], P[1], P[2], P[3]);
-        fw[nx + c] = former_f(nx + c, N, P[13], P[14], P[1], P[2], P[3]);
-      }
+      const int c = min(lane + TPB * t, nx - 1);
+      C.fxr[t] = former_f(c, N, P[13], P[14], P[1], P[2], P[3]);
+      C.fur[t] = former_f(nx + c, N, P[13], P[14], P[1], P[2], P[3]);
     }
 #pragma unroll
     for (int t = 0; t < Lo::SE; ++t) {
       const auto q = RegCtx<N>::erow(lane, t);
-      if (q.valid) bw[q.e] = former_b(q.e, N, F);
+      C.bvr[t] = former_b(q.valid ? q.e : 0, N, F);
     }
 #pragma unroll
-    for (int t = 0; t < SI; ++t)
-      if (lane + TPB * t < m) dw[lane + TPB * t] = former_d(lane + TPB * t, N, P[2], P[12], mu);
-    // each entry is re-read only by the lane that wrote it: workgroup scope orders that (a device-
-    // scope release would write back L2)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    C.fg = fw;
-    C.bg = bw;
-    C.hg = dw;
-    C.load_qp_vectors();  // same lanes, same entries as written above: no other wave involved
+    for (int t = 0; t < SI; ++t) C.hvr[t] = former_d(min(lane + TPB * t, m - 1), N, P[2], P[12], mu);
+    if (fa.vec[0]) {
+      double* fw = fa.vec[0] + (size_t)env * nz;
+#pragma unroll
+      for (int t = 0; t < Lo::SX; ++t)
+        if (lane + TPB * t < nx) {
+          fw[lane + TPB * t] = C.fxr[t];
+          fw[nx + lane + TPB * t] = C.fur[t];
+        }
+    }
+    if (fa.vec[1]) {
+      double* bw = fa.vec[1] + (size_t)env * p;
+#pragma unroll
+      for (int t = 0; t < Lo::SE; ++t) {
+        const auto q = RegCtx<N>::erow(lane, t);
+        if (q.valid) bw[q.e] = C.bvr[t];
+      }
+    }
+    if (fa.vec[2]) {
+      double* dw = fa.vec[2] + (size_t)env * m;
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (lane + TPB * t < m) dw[lane + TPB * t] = C.hvr[t];
+    }
   } else {
     const int nA = nnz_A(N), nG = 28 * N;
     const double* Hg = solver_in(args, 0) + (size_t)env * nz;
@@ -1207,7 +1250,21 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   // that loop before X is written (one wave runs both loops in order)
   if constexpr (TPB > 64) __syncthreads();
   double *X = smem + Lo::X, *Z = smem + Lo::Z, *Y = smem + Lo::Y;
-  if (!kFused && args.init_mode == 0) {
+  if (!kFused && args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
+    const double* xg = solver_in(args, 6) + (size_t)env * nz;
+    for (int e = lane; e < nz; e += TPB) X[e] = xg[e];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + TPB * t;
+      if (q < m) {
+        C.s[t] = fmax(C.hvr[t] - ccs_gx(solver_in(args, 1) + (size_t)env * 28 * N, q, X + nx), 1.0);
+        C.z[t] = 1.0;
+        Z[q] = 1.0;
+      }
+    }
+    for (int e = lane; e < p; e += TPB) Y[e] = 0.0;
+  } else if (!kFused && args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;
@@ -1325,28 +1382,58 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   }
   PROF_FLUSH(C);
   auto outp = [&](int k) { return kFused ? fa.out[k] : solver_out(args, k); };
-  double* xo = outp(0) + (size_t)env * nz;
-  double* so = outp(1) + (size_t)env * m;
-  double* zo = outp(2) + (size_t)env * m;
-  double* yo = outp(3) + (size_t)env * p;
-  double* ro = outp(4) + (size_t)env * 4;
-  double* mo = outp(5) + (size_t)env;
-  for (int e = lane; e < nz; e += TPB) xo[e] = X[e];
+  if (double* xo = outp(0)) {
+    xo += (size_t)env * nz;
+    for (int e = lane; e < nz; e += TPB) xo[e] = X[e];
+  }
+  double* so = outp(1);
+  double* zo = outp(2);
 #pragma unroll
   for (int t = 0; t < SI; ++t) {
     const int q = lane + TPB * t;
     if (q < m) {
-      so[q] = C.s[t];
-      zo[q] = C.z[t];
+      if (so) so[(size_t)env * m + q] = C.s[t];
+      if (zo) zo[(size_t)env * m + q] = C.z[t];
     }
   }
-  for (int e = lane; e < p; e += TPB) yo[e] = Y[e];
+  if (double* yo = outp(3)) {
+    yo += (size_t)env * p;
+    for (int e = lane; e < p; e += TPB) yo[e] = Y[e];
+  }
   if (lane == 0) {
-    ro[0] = res0;
-    ro[1] = res1;
-    ro[2] = res2;
-    ro[3] = mu_new;
-    mo[0] = mu_new;
+    if (double* ro = outp(4)) {
+      ro += (size_t)env * 4;
+      ro[0] = res0;
+      ro[1] = res1;
+      ro[2] = res2;
+      ro[3] = mu_new;
+    }
+    if (double* mo = outp(5)) mo[env] = mu_new;
+  }
+  if constexpr (kFused) {
+    if (fa.wrench) {  // u0 -> foot wrench (+ stance torque): srbd_u0_wrench_torque's arithmetic
+      const float* Rm = fa.prep.rotation_body + 9 * (size_t)env;
+      float* wl = reinterpret_cast<float*>(smem + Lo::TV);  // TV is dead after the last update
+      if (lane < 12) {
+        const float w = wrench_entry(X + nx, Rm, lane);
+        fa.wrench[(size_t)env * 12 + lane] = w;
+        wl[lane] = w;
+      }
+      if (fa.tau) {
+        __syncthreads();
+        const int nd = fa.ndof;
+        for (int q = lane; q < 2 * nd; q += TPB) {
+          const int l = q / nd, k = q - l * nd;
+          const float* Jl = fa.jac + ((size_t)env * 2 + l) * 6 * nd;
+          float t = 0.0f;
+          if (fa.contact[(size_t)env * 2 + l] != 0.0f) {
+            t = fm(Jl[k], wl[6 * l]);
+            for (int j = 1; j < 6; ++j) t = fa_(t, fm(Jl[j * nd + k], wl[6 * l + j]));
+          }
+          fa.tau[((size_t)env * 2 + l) * nd + k] = t;
+        }
+      }
+    }
   }
 }
 

@@ -18,6 +18,7 @@
 #include "qp_former.hpp"
 #include "mpc_io.hpp"
 #include "reg20.hpp"
+#include "device_state.hpp"
 
 namespace {
 
@@ -33,6 +34,7 @@ int set_error(int code, const char* what) {
 
 constexpr int kFormerWaves = 4;
 constexpr int kErrInvalid = (int)hipErrorInvalidValue;
+constexpr int kFallbackGrid = 512;
 
 bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 
@@ -42,17 +44,29 @@ constexpr size_t kRegLds10 = sizeof(double) * (size_t)srbd::RegLayout<10>::total
 constexpr size_t kRegLds20 = sizeof(double) * (size_t)srbd::RegLayout<20>::total;
 static_assert(kRegLds10 <= 20 * 1024, "N=10 register kernel must fit 8 QPs per CU");
 
-// 0 = auto (stage-invariant kernels -- register-resident for N = 10 and 20, LDS-resident otherwise -- and
-// the general kernel for flagged QPs); 1 = general kernel only; 2 = LDS-resident fast kernel
-int g_solver_path = 0;
+// The HIP device current at this call (-1 if none / out of range for the per-device state)
+int current_device() {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= srbd::kMaxDevices) return -1;
+  return d;
+}
 
-int ensure_lds_attr(const void* fn, size_t bytes, size_t* configured) {
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lock(mu);
-  if (bytes <= *configured) return 0;
+// Solver path per device: 0 = auto (stage-invariant kernels -- register-resident for N = 10 and 20,
+// LDS-resident otherwise -- and the general kernel for flagged QPs); 1 = general kernel only;
+// 2 = LDS-resident fast kernel. Selected by srbd_set_solver_path for the current device.
+srbd::PerDevice<int> g_solver_path;
+int solver_path() {
+  const int* p = g_solver_path.at(current_device());
+  return p ? *p : 0;
+}
+
+int ensure_lds_attr(const void* fn, size_t bytes, srbd::LdsAttr& cache) {
+  const int dev = current_device();
+  if (dev < 0) return set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
+  if (!cache.claim(dev, bytes)) return 0;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   if (e != hipSuccess) return set_error((int)e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
-  *configured = bytes;
+  cache.commit(dev, bytes);
   return 0;
 }
 
@@ -66,33 +80,34 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
-  static size_t cfg_general = 0, cfg_fast = 0, cfg_fast10 = 0, cfg_fast20 = 0, cfg_reg10 = 0, cfg_reg20 = 0;
+  static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20, cfg_reg10, cfg_reg20;
   srbd::SolverArgs a = a0;
   a.only_flagged = 0;
-  if (g_solver_path == 0 && (a.N == 10 || a.N == 20)) {
+  const int path = solver_path();
+  if (path == 0 && (a.N == 10 || a.N == 20)) {
     if (a.N == 10) {
-      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, &cfg_reg10)) return rc;
+      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, cfg_reg10)) return rc;
       hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
     } else {
 #ifdef SRBD_SPLIT_REG20
-      if (int rc = ensure_lds_attr(srbd::reg20::solver_kernel(), kRegLds20, &cfg_reg20)) return rc;
+      if (int rc = ensure_lds_attr(srbd::reg20::solver_kernel(), kRegLds20, cfg_reg20)) return rc;
       srbd::reg20::launch_solver(a, kRegLds20, s);
 #else
-      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, &cfg_reg20)) return rc;
+      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, cfg_reg20)) return rc;
       hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, s, a);
 #endif
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
     a.only_flagged = 1;
-  } else if (g_solver_path == 0 || g_solver_path == 2) {
+  } else if (path == 0 || path == 2) {
     const size_t lds = fast_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
     // horizon-specialised instantiations for the common horizons, runtime-N otherwise
     const void* fn = a.N == 10 ? (const void*)srbd::pdipm_srbd_kernel<10>
                    : a.N == 20 ? (const void*)srbd::pdipm_srbd_kernel<20>
                                : (const void*)srbd::pdipm_srbd_kernel<0>;
-    size_t* cfg = a.N == 10 ? &cfg_fast10 : a.N == 20 ? &cfg_fast20 : &cfg_fast;
+    srbd::LdsAttr& cfg = a.N == 10 ? cfg_fast10 : a.N == 20 ? cfg_fast20 : cfg_fast;
     if (int rc = ensure_lds_attr(fn, lds, cfg)) return rc;
     if (a.N == 10) hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<10>, dim3(a.batch), dim3(64), lds, s, a);
     else if (a.N == 20) hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<20>, dim3(a.batch), dim3(64), lds, s, a);
@@ -103,35 +118,47 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   }
   const size_t lds = solver_lds_bytes(a.N);
   if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
-  if (int rc = ensure_lds_attr((const void*)srbd::pdipm_kernel, lds, &cfg_general)) return rc;
-  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(64), lds, s, a);
+  if (int rc = ensure_lds_attr((const void*)srbd::pdipm_kernel, lds, cfg_general)) return rc;
+  // the fallback pass walks the batch with a bounded grid and solves only the flagged QPs (none for
+  // qp_former output): a few hundred short workgroups instead of one large-LDS workgroup per QP
+  const int grid = a.only_flagged ? (a.batch < kFallbackGrid ? a.batch : kFallbackGrid) : a.batch;
+  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(grid), dim3(64), lds, s, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "pdipm_kernel launch");
 }
 
-// CusADi-style blocking call on the legacy default stream, timed with hipEvents.
+// CusADi-style blocking call on the legacy default stream, timed with hipEvents (one event pair
+// per device, created on first use there; the reference creates and leaks two per call).
 template <class F>
 float timed_blocking(F&& launch) {
+  struct Events {
+    hipEvent_t ev[2];
+  };
   static std::mutex mu;
-  static hipEvent_t ev0 = nullptr, ev1 = nullptr;  // created once (the reference leaks 2 per call)
+  static srbd::PerDevice<Events> events;
   std::lock_guard<std::mutex> lock(mu);
-  if (!ev0) {
-    if (hipEventCreate(&ev0) != hipSuccess || hipEventCreate(&ev1) != hipSuccess) {
+  Events* ev = events.at(current_device());
+  if (!ev) {
+    set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
+    return -1.0f;
+  }
+  if (!ev->ev[0]) {
+    if (hipEventCreate(&ev->ev[0]) != hipSuccess || hipEventCreate(&ev->ev[1]) != hipSuccess) {
       set_error((int)hipErrorInitializationError, "hipEventCreate");
       return -1.0f;
     }
   }
-  (void)hipEventRecord(ev0, 0);
+  (void)hipEventRecord(ev->ev[0], 0);
   if (launch() != 0) return -1.0f;
-  (void)hipEventRecord(ev1, 0);
-  hipError_t e = hipEventSynchronize(ev1);
+  (void)hipEventRecord(ev->ev[1], 0);
+  hipError_t e = hipEventSynchronize(ev->ev[1]);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     set_error((int)e, "kernel execution");
     return -1.0f;
   }
   float ms = 0.0f;
-  (void)hipEventElapsedTime(&ms, ev0, ev1);
+  (void)hipEventElapsedTime(&ms, ev->ev[0], ev->ev[1]);
   return ms / 1000.0f;
 }
 
@@ -158,7 +185,9 @@ int srbd_debug_phase_cycles(unsigned long long* out16) {
 int srbd_set_solver_path(int path) {
   if (path < 0 || path > 2)
     return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto), 1 (general) or 2 (LDS-resident fast)");
-  g_solver_path = path;
+  int* p = g_solver_path.at(current_device());
+  if (!p) return set_error((int)hipErrorInvalidDevice, "srbd_set_solver_path: no current HIP device");
+  *p = path;
   return 0;
 }
 
@@ -225,7 +254,7 @@ static int pdipm_common(int horizon, int n_iter, int batch, double y0, int init_
     return set_error(kErrInvalid, "srbd_pdipm: bad arguments");
   if (batch == 0) return 0;
   srbd::SolverArgs a{};
-  const int nin = init_mode ? 6 : 10;
+  const int nin = init_mode == 0 ? 10 : init_mode == 2 ? 7 : 6;  // QP + iterate / + x_init / QP only
   for (int i = 0; i < nin; ++i) {
     if (!inputs[i]) return set_error(kErrInvalid, "srbd_pdipm: null input");
     a.in[i] = inputs[i];
@@ -252,6 +281,12 @@ int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double*
   return pdipm_common(horizon, n_iter, batch, y0, 1, inputs, outputs, stream);
 }
 
+int srbd_pdipm_ccs(int horizon, int n_iter, int batch, const double* const* inputs, double* const* outputs,
+                   void* stream) {
+  if (!inputs || (batch > 0 && !inputs[6])) return set_error(kErrInvalid, "srbd_pdipm_ccs: null x_init");
+  return pdipm_common(horizon, n_iter, batch, 0.0, 2, inputs, outputs, stream);
+}
+
 int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                    double* qp_workspace, double* const* outputs, void* stream) {
   if (!horizon_ok(horizon) || !qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve: bad arguments");
@@ -268,11 +303,32 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
   return srbd_pdipm_cold(horizon, n_iter, batch, y0, sin, outputs, stream);
 }
 
+// launch of the fused / controller-step kernel (a fully set up FusedArgs)
+static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
+  static srbd::LdsAttr cfg10, cfg20;
+  if (a.N == 10) {
+    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, cfg10)) return rc;
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, st, a);
+  } else {
+#ifdef SRBD_SPLIT_REG20
+    if (int rc = ensure_lds_attr(srbd::reg20::step_kernel(), kRegLds20, cfg20)) return rc;
+    srbd::reg20::launch_step(a, kRegLds20, st);
+#else
+    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, cfg20)) return rc;
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, st, a);
+#endif
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");
+}
+
 int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                          double* qp_workspace, double* const* outputs, void* stream) {
-  if (!(horizon == 10 || horizon == 20) || g_solver_path != 0)  // no fused kernel: former + solver
+  if (!(horizon == 10 || horizon == 20) || solver_path() != 0) {  // no fused kernel: former + solver
+    if (!qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve_fused: this horizon / solver path needs qp_workspace");
     return srbd_mpc_solve(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, stream);
-  if (n_iter < 1 || batch < 0 || !former_inputs || !qp_workspace || !outputs)
+  }
+  if (n_iter < 1 || batch < 0 || !former_inputs || !outputs)
     return set_error(kErrInvalid, "srbd_mpc_solve_fused: bad arguments");
   if (batch == 0) return 0;
   const size_t N = (size_t)horizon, B = (size_t)batch;
@@ -281,36 +337,93 @@ int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const do
     if (!former_inputs[i]) return set_error(kErrInvalid, "srbd_mpc_solve_fused: null input");
     a.in[i] = former_inputs[i];
   }
-  for (int i = 0; i < 6; ++i) {
-    if (!outputs[i]) return set_error(kErrInvalid, "srbd_mpc_solve_fused: null output");
-    a.out[i] = outputs[i];
+  for (int i = 0; i < 6; ++i) a.out[i] = outputs[i];  // null: not written
+  if (qp_workspace) {  // same slots as srbd_mpc_solve's H, f, A, b, G, d
+    a.vec[0] = qp_workspace + B * 24 * N;
+    a.vec[1] = a.vec[0] + B * 24 * N + B * (122 * N - 24);
+    a.vec[2] = a.vec[1] + B * 14 * N + B * 28 * N;
   }
-  double* f = qp_workspace + B * 24 * N;   // same slots as srbd_mpc_solve's H, f, A, b, G, d
-  double* b = f + B * 24 * N + B * (122 * N - 24);
-  double* d = b + B * 14 * N + B * 28 * N;
-  a.vec[0] = f;
-  a.vec[1] = b;
-  a.vec[2] = d;
   a.N = horizon;
   a.n_iter = n_iter;
   a.batch = batch;
   a.y0 = y0;
-  static size_t cfg10 = 0, cfg20 = 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (horizon == 10) {
-    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, &cfg10)) return rc;
-    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(batch), dim3(64), kRegLds10, st, a);
-  } else {
-#ifdef SRBD_SPLIT_REG20
-    if (int rc = ensure_lds_attr(srbd::reg20::step_kernel(), kRegLds20, &cfg20)) return rc;
-    srbd::reg20::launch_step(a, kRegLds20, st);
-#else
-    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, &cfg20)) return rc;
-    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(batch), dim3(srbd::reg_tpb(20)), kRegLds20, st, a);
-#endif
+  return launch_step(a, (hipStream_t)stream);
+}
+
+// srbd_mpc_prep (host struct of device pointers + constants) -> the kernels' PrepArgs
+static int fill_prep(const srbd_mpc_prep* p, srbd::PrepArgs& a, const char* who) {
+  if (!p->root_euler || !p->root_position || !p->root_angular_velocity_w || !p->root_velocity_w ||
+      !p->rotation_body || !p->foot_position || !p->desired_velocity_b || !p->desired_angular_velocity_b ||
+      !p->desired_height || !p->world_position_desired || !p->yaw_desired || !p->first_run || !p->dt_mpc ||
+      !p->residual_lin_accel || !p->residual_ang_accel ||
+      (p->gait_phase ? (!p->ssp_durations || !p->dsp_durations) : !p->contact_table) ||
+      (p->q_len != 12 && p->q_len != 13)) {
+    std::string w = std::string(who) + ": missing array or bad q_len";
+    return set_error(kErrInvalid, w.c_str());
   }
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");
+  a.root_euler = p->root_euler;
+  a.root_position = p->root_position;
+  a.ang_vel_w = p->root_angular_velocity_w;
+  a.vel_w = p->root_velocity_w;
+  a.rotation_body = p->rotation_body;
+  a.foot_position = p->foot_position;
+  a.des_vel_b = p->desired_velocity_b;
+  a.des_angvel_b = p->desired_angular_velocity_b;
+  a.des_height = p->desired_height;
+  a.wpd = p->world_position_desired;
+  a.yaw_des = p->yaw_desired;
+  a.first_run = p->first_run;
+  a.gait_phase = p->gait_phase;
+  a.ssp = p->ssp_durations;
+  a.dsp = p->dsp_durations;
+  a.contact_table = p->contact_table;
+  a.dt_mpc = p->dt_mpc;
+  a.res_lin = p->residual_lin_accel;
+  a.res_ang = p->residual_ang_accel;
+  std::memcpy(a.I_body, p->I_body, sizeof(a.I_body));
+  a.mass = p->mass;
+  a.mu = p->mu;
+  std::memcpy(a.Q, p->Q, sizeof(a.Q));
+  a.q_len = p->q_len;
+  std::memcpy(a.R, p->R, sizeof(a.R));
+  a.step_dt = p->step_dt;
+  a.literal = p->literal_layout ? 1 : 0;
+  return 0;
+}
+
+int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
+                  double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
+                  const float* contact_jacobian, const float* contact_bool, float* tau, void* stream) {
+  if (!(horizon == 10 || horizon == 20))
+    return set_error(kErrInvalid, "srbd_mpc_step: horizon 10 or 20 (other horizons: srbd_prepare_inputs + "
+                                  "srbd_mpc_solve + srbd_u0_wrench_torque)");
+  if (n_iter < 1 || batch < 0 || !prep || (tau && (ndof < 1 || ndof > 64)))
+    return set_error(kErrInvalid, "srbd_mpc_step: bad arguments");
+  if (batch == 0) return 0;
+  if (!foot_wrench || (tau && (!contact_jacobian || !contact_bool)))
+    return set_error(kErrInvalid, "srbd_mpc_step: null foot_wrench / contact_jacobian / contact_bool");
+  srbd::FusedArgs a{};
+  if (int rc = fill_prep(prep, a.prep, "srbd_mpc_step")) return rc;
+  a.prep.N = horizon;
+  a.prep.batch = batch;
+  if (former_inputs)
+    for (int i = 0; i < 17; ++i) {
+      if (!former_inputs[i]) return set_error(kErrInvalid, "srbd_mpc_step: null former_inputs entry");
+      a.prep.out[i] = former_inputs[i];
+    }
+  a.ctrl = 1;
+  if (outputs)
+    for (int i = 0; i < 6; ++i) a.out[i] = outputs[i];
+  a.wrench = foot_wrench;
+  a.tau = tau;
+  a.jac = contact_jacobian;
+  a.contact = contact_bool;
+  a.ndof = tau ? ndof : 0;
+  a.N = horizon;
+  a.n_iter = n_iter;
+  a.batch = batch;
+  a.y0 = y0;
+  return launch_step(a, (hipStream_t)stream);
 }
 
 int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind) {
@@ -378,41 +491,8 @@ int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* p, double* 
   if (!horizon_ok(horizon) || batch < 0 || !p || !former_inputs)
     return set_error(kErrInvalid, "srbd_prepare_inputs: bad arguments");
   if (batch == 0) return 0;
-  if (!p->root_euler || !p->root_position || !p->root_angular_velocity_w || !p->root_velocity_w ||
-      !p->rotation_body || !p->foot_position || !p->desired_velocity_b || !p->desired_angular_velocity_b ||
-      !p->desired_height || !p->world_position_desired || !p->yaw_desired || !p->first_run || !p->dt_mpc ||
-      !p->residual_lin_accel || !p->residual_ang_accel ||
-      (p->gait_phase ? (!p->ssp_durations || !p->dsp_durations) : !p->contact_table) ||
-      (p->q_len != 12 && p->q_len != 13))
-    return set_error(kErrInvalid, "srbd_prepare_inputs: missing array or bad q_len");
   srbd::PrepArgs a{};
-  a.root_euler = p->root_euler;
-  a.root_position = p->root_position;
-  a.ang_vel_w = p->root_angular_velocity_w;
-  a.vel_w = p->root_velocity_w;
-  a.rotation_body = p->rotation_body;
-  a.foot_position = p->foot_position;
-  a.des_vel_b = p->desired_velocity_b;
-  a.des_angvel_b = p->desired_angular_velocity_b;
-  a.des_height = p->desired_height;
-  a.wpd = p->world_position_desired;
-  a.yaw_des = p->yaw_desired;
-  a.first_run = p->first_run;
-  a.gait_phase = p->gait_phase;
-  a.ssp = p->ssp_durations;
-  a.dsp = p->dsp_durations;
-  a.contact_table = p->contact_table;
-  a.dt_mpc = p->dt_mpc;
-  a.res_lin = p->residual_lin_accel;
-  a.res_ang = p->residual_ang_accel;
-  std::memcpy(a.I_body, p->I_body, sizeof(a.I_body));
-  a.mass = p->mass;
-  a.mu = p->mu;
-  std::memcpy(a.Q, p->Q, sizeof(a.Q));
-  a.q_len = p->q_len;
-  std::memcpy(a.R, p->R, sizeof(a.R));
-  a.step_dt = p->step_dt;
-  a.literal = p->literal_layout ? 1 : 0;
+  if (int rc = fill_prep(p, a, "srbd_prepare_inputs")) return rc;
   for (int i = 0; i < 17; ++i) {
     if (!former_inputs[i]) return set_error(kErrInvalid, "srbd_prepare_inputs: null output");
     a.out[i] = former_inputs[i];

@@ -84,14 +84,15 @@ class ShardedMPC:
     def step_async(self, local_inputs: Sequence[torch.Tensor]) -> "PendingGather":
         """Like ``step`` but the u0 gather is left running on the collective's own stream (RCCL),
         so it overlaps the next step's solve; ``.wait()`` on the returned handle yields u0 of every
-        env. Two steps' gathers may be in flight; a handle must be waited before the step after
-        next reuses its buffers (``PendingGather.wait`` is idempotent)."""
+        env as a tensor of its own (later steps never overwrite it). Two steps' gathers may be in
+        flight: the step after next waits for this one before reusing its send / receive pair
+        (``PendingGather.wait`` is idempotent)."""
         if local_inputs[0].shape[0] != self.local_envs:
             raise ValueError(f"rank {self.rank}: expected {self.local_envs} envs, got {local_inputs[0].shape[0]}")
         self.x_local = self._solve(local_inputs)
         u0 = self.x_local[:, 12 * self.N:12 * self.N + 12]
-        if self.world == 1:
-            return PendingGather(u0, None, None)
+        if self.world == 1:  # the next solve reuses x_local: hand out a copy (96 B/env)
+            return PendingGather(u0.clone(), None, None)
         if self._abuf is None:
             mk = lambda *sh: torch.zeros(sh, dtype=torch.float64, device=self.device)  # noqa: E731
             self._abuf = [(mk(self.slot, 12), mk(self.world * self.slot, 12)) for _ in range(2)]
@@ -146,5 +147,6 @@ class PendingGather:
         if self._out is None:
             if self._work is not None:
                 self._work.wait()  # the current stream now waits for the collective
-            self._out = self._buf if self._keep is None else self._buf.index_select(0, self._keep)
+            # a copy: the receive buffer is reused by the gather two steps later
+            self._out = self._buf.clone() if self._keep is None else self._buf.index_select(0, self._keep)
         return self._out

@@ -79,6 +79,26 @@ def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_
     return outputs
 
 
+def pdipm_ccs(qp: list[torch.Tensor], x_init: torch.Tensor, N: int, n_iter: int,
+              outputs: list[torch.Tensor] | None = None):
+    """The reference's ``_ccs`` solver (sparse_pdipm_solver_ccs, sparse_pdipm_solver.py:4-35): n_iter
+    Mehrotra iterations from x = x_init, s = max(h - G x_init, 1), z = 1, y = 0
+    (initialize_pdipm_variables, :537-558). qp: [Q_val, G_val, A_val, f, h, b]; x_init (B, 24N).
+    Returns [x, s, z, y, residuals(4), mu(1)] (the reference Function returns x)."""
+    d = Dims(N)
+    B = qp[0].shape[0]
+    ins = list(qp) + [x_init, None, None, None]
+    _check_batch(ins, d.solver_in_nnz, B, "pdipm_ccs")
+    if outputs is None:
+        outputs = _alloc_solver_outputs(B, N, qp[0].device)
+    _check_batch(outputs, d.solver_out_nnz, B, "pdipm_ccs outputs")
+    rc = _native.lib().srbd_pdipm_ccs(N, n_iter, B, _native.ptr_array([t.data_ptr() if t is not None else 0
+                                                                       for t in ins]),
+                                      _native.ptr_array([t.data_ptr() for t in outputs]), _stream_ptr())
+    _native.check(rc, "srbd_pdipm_ccs")
+    return outputs
+
+
 @dataclass
 class MPCSolveBuffers:
     """Preallocated device buffers for repeated ``mpc_solve`` calls (no allocation per step)."""
@@ -104,14 +124,15 @@ class MPCSolveBuffers:
 
 
 def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float = 1.0,
-              buffers: MPCSolveBuffers | None = None, fused: bool = True):
+              buffers: MPCSolveBuffers | None = None, fused: bool = True, keep_qp: bool = False):
     """qp_former + cold-started PDIPM in one stream with no host synchronisation.
 
     Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
     iteration count as a runtime argument. Returns [x, s, z, y, residuals, mu].
-    ``fused`` (default): for N = 10 and 20 one kernel forms the QP's stage blocks in LDS and solves
-    it (``srbd_mpc_solve_fused``; only f, b, d reach ``buffers.workspace``); ``False`` runs the
-    former and the solver as two kernels with the full QP in the workspace.
+    ``fused`` (default): for N = 10 and 20 one kernel forms the QP in registers / LDS and solves it
+    (``srbd_mpc_solve_fused``): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to
+    their ``buffers.workspace`` slots); ``False`` runs the former and the solver as two kernels
+    with the full QP in the workspace.
     """
     d = Dims(N)
     B = former_inputs[0].shape[0]
@@ -124,7 +145,7 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     L = _native.lib()
     rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
                           _native.ptr_array([t.data_ptr() for t in former_inputs]),
-                          buffers.workspace.data_ptr(),
+                          buffers.workspace.data_ptr() if (keep_qp or not fused or N not in (10, 20)) else None,
                           _native.ptr_array([t.data_ptr() for t in buffers.outputs]), _stream_ptr())
     _native.check(rc, "srbd_mpc_solve")
     return buffers.outputs

@@ -162,3 +162,33 @@ def solver_init(d_vec: np.ndarray, N: int, y0: float = 1.0):
     z = np.ones((B, dims.n_ineq))
     y = np.full((B, dims.n_eq), y0)
     return x, s, z, y
+
+
+def make_controller(B: int, N: int = 10, seed: int = 0, device="cuda", n_iter: int = 10):
+    """An MPCControllerHIP over B synthetic robots (float32 state estimate / command / gait as the
+    reference data classes hold them, SURVEY 8d distributions, device-side gait schedule): the
+    controller-step workload of bench.py."""
+    import torch
+
+    from biped_pympc_amd.controller import DesiredStateData, MPCConf, MPCControllerHIP, StateEStimatorData
+    rng = np.random.default_rng(seed)
+    eul = np.stack([rng.uniform(-0.15, 0.15, B), rng.uniform(-0.15, 0.15, B), rng.uniform(-math.pi, math.pi, B)], 1)
+    R = rot_zyx(eul[:, 0], eul[:, 1], eul[:, 2])
+    pos = np.stack([rng.uniform(-1, 1, B), rng.uniform(-1, 1, B), 0.55 + rng.uniform(-0.03, 0.03, B)], 1)
+    feet = np.stack([pos + np.einsum("bij,j->bi", R, [0.0, 0.10, -0.55]),
+                     pos + np.einsum("bij,j->bi", R, [0.0, -0.10, -0.55])], 1)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device)  # noqa: E731
+    c = MPCControllerHIP(B, device, 2, MPCConf(horizon_length=N, pdipm_iterations=n_iter))
+    se = StateEStimatorData(2, B, device)
+    se.root_euler, se.root_position, se.rotation_body, se.foot_position = f32(eul), f32(pos), f32(R), f32(feet)
+    se.root_angular_velocity_w = f32(rng.normal(0, 0.2, (B, 3)))
+    se.root_velocity_w = f32(rng.normal(0, 0.3, (B, 3)))
+    ds = DesiredStateData(B, device)
+    ds.desired_velocity_b = f32(np.stack([rng.uniform(-1, 1, B), rng.uniform(-1, 1, B), np.zeros(B)], 1))
+    ds.desired_angular_velocity_b = f32(np.stack([np.zeros(B), np.zeros(B), rng.uniform(-1, 1, B)], 1))
+    ds.desired_height = f32(0.55 + rng.uniform(-0.02, 0.02, B))
+    c.set_state_estimate_data(se)
+    c.set_desired_state_data(ds)
+    c.set_gait(torch.from_numpy(rng.uniform(0, 1, B).astype(np.float32)),
+               torch.from_numpy(rng.integers(3, 7, (B, 2))), torch.from_numpy(rng.integers(0, 3, (B, 2))))
+    return c

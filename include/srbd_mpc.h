@@ -66,6 +66,13 @@ int srbd_pdipm(int horizon, int n_iter, int batch, const double* const* inputs,
 int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double* const* inputs,
                     double* const* outputs, void* stream);
 
+/* The reference's `_ccs` solver entry (sparse_pdipm_solver_ccs, sparse_pdipm_solver.py:4-35, and
+ * initialize_pdipm_variables :537-558): the iterate starts from an arbitrary primal guess,
+ * x = x_init (input 6), s = max(h - G x_init, 1), z = 1, y = 0; inputs 7..9 unused (may be NULL).
+ * The reference Function returns x only; here all 6 outputs as srbd_pdipm. */
+int srbd_pdipm_ccs(int horizon, int n_iter, int batch, const double* const* inputs, double* const* outputs,
+                   void* stream);
+
 /* Whole MPC QP step: qp_former -> cold-start PDIPM (n_iter iterations), one stream, no host sync.
  * `qp_workspace` is caller-owned device memory of srbd_mpc_workspace_doubles(horizon, batch)
  * doubles that receives H, f, A, b, G, d (CCS, batched). outputs as srbd_pdipm. */
@@ -74,9 +81,10 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
                    double* qp_workspace, double* const* outputs, void* stream);
 
 /* srbd_mpc_solve in ONE kernel for N = 10 and 20 (other horizons, or a non-auto solver path, run
- * srbd_mpc_solve): the stage blocks of H, A, G are computed in the solver from the former inputs
- * and never written; f, b, d are written to their slots of the same qp_workspace and H, A, G slots
- * are left untouched. Same outputs as srbd_mpc_solve. */
+ * srbd_mpc_solve and need qp_workspace): the QP is formed in the solver from the former inputs and
+ * never written, except f, b, d into their qp_workspace slots when qp_workspace != NULL (NULL: no
+ * QP data leaves the kernel). Same outputs as srbd_mpc_solve; any outputs[k] may be NULL (that
+ * output is not written). */
 int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                          double* qp_workspace, double* const* outputs, void* stream);
 
@@ -87,7 +95,13 @@ size_t srbd_solver_lds_bytes(int horizon);
  * (every QP qp_former emits; register-resident at N = 10 and 20, LDS-resident otherwise), the general
  * kernel for any other QP in the batch; 1 = general kernel only; 2 = LDS-resident stage-invariant
  * kernel at every horizon (plus the general fallback).
- * Results agree to round-off (tests/test_gpu_parity.py). Process-wide. */
+ * Results agree to round-off (tests/test_gpu_parity.py). Per device: applies to calls made while
+ * the current HIP device is the one current here.
+ *
+ * Devices: every entry point works on the HIP device current at the call (one process per GPU is
+ * the deployment model; a process that switches devices is supported too). What the
+ * library keeps between calls -- configured kernel LDS limits, the blocking calls' events, the
+ * solver path -- is kept per device (csrc/device_state.hpp). */
 int srbd_set_solver_path(int path);
 
 /* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
@@ -139,6 +153,21 @@ typedef struct srbd_mpc_prep {
  * inputs (FP64, (B, nnz_in[i]), Q well-formed 12 wide) and updates the knot-point state. */
 int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* prep, double* const* former_inputs,
                         void* stream);
+
+/* The whole controller step in ONE kernel launch (N = 10 and 20): srbd_prepare_inputs' arithmetic
+ * computes this env's 17 former inputs into on-chip memory (and advances the knot-point state in
+ * prep), the fused former + cold PDIPM (n_iter iterations, y = y0) solves, and
+ * srbd_u0_wrench_torque's arithmetic writes foot_wrench (B,2,6) float32 -- and tau (B,2,ndof) when
+ * tau != NULL, from contact_jacobian (B,2,6,ndof) / contact_bool (B,2). former_inputs (host array
+ * of 17 device pointers as srbd_prepare_inputs) may be NULL: the prepared inputs then never leave
+ * the chip. outputs (host array of 6 device pointers as srbd_pdipm) may be NULL, and each entry
+ * may be NULL: the step then writes only the wrench (48 B/env). Bit-identical to srbd_prepare_inputs -> srbd_mpc_solve_fused ->
+ * srbd_u0_wrench_torque. Replaces MPCControllerCusadi.run (mpc_controller_cusadi.py:43-205) with
+ * BaseMPCController's preparation (base_controller.py:166-257) and LegController.update_ff_torque
+ * (leg_controller.py:87-95). */
+int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
+                  double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
+                  const float* contact_jacobian, const float* contact_bool, float* tau, void* stream);
 
 /* u0 = x[:, 12N:12N+12] -> foot wrench (B,2,6) float32 in the body frame, x-moments zeroed and
  * negated as mpc_controller_cusadi.py:186-203. rotation_body (B,3,3) float32 row-major. */

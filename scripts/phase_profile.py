@@ -42,8 +42,9 @@ e1.record()
 torch.cuda.synchronize()
 L.srbd_debug_phase_cycles(acc)
 names = ["residuals", "factor: parallel (W, Phi_u blocks, S_ii)", "factor: stage chain (Schur + sweep)",
-         "solve: parallel parts (x2)", "solve: fwd/bwd chains (x2)", "step lengths / update"]
-tot = sum(acc[k] for k in range(6))
+         "solve: parallel parts (x3)", "solve: fwd/bwd chains (x3)", "step lengths / update",
+         "refinement residuals (KKT rows 1, 4)"]
+tot = sum(acc[k] for k in range(7))
 print(f"N={N} B={B} K={K}: step {e0.elapsed_time(e1):.3f} ms; cycles per QP per iteration:")
 for k, n in enumerate(names):
     print(f"  {n:45s} {acc[k] / B / K:10.0f}  ({100 * acc[k] / tot:5.1f} %)")

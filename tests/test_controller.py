@@ -306,3 +306,68 @@ def test_graphed_step_replays_the_controller_step():
         for c in (c1, c2):
             c.state_estimate_data.root_position.add_(0.01)
             c.state_estimate_data.foot_position.add_(0.01)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,gait,literal,torque", [(10, True, True, False), (10, False, True, True),
+                                                   (20, True, False, True), (10, True, True, True)])
+def test_one_launch_step_equals_three_kernels(N, gait, literal, torque):
+    """srbd_mpc_step (prep -> fused former + PDIPM -> wrench / torque in ONE kernel, inputs kept
+    on chip) against the three-launch sequence it replaces: wrench, torque, solution and the
+    advanced knot-point state bit for bit, over three consecutive steps."""
+    B, ndof = 77, 6
+    st, cmd, ctrl, params, gait_args, table = random_robot(B, 41 + N, N, gait=gait)
+    c1 = _controller(B, N, st, cmd, ctrl, params, gait_args, table, literal)
+    c2 = _controller(B, N, st, cmd, ctrl, params, gait_args, table, literal)
+    c1.cfg.keep_solution = True
+    J, cb = (torch.from_numpy(a) for a in _torque_inputs(B, ndof, 9))
+    for step in range(3):
+        if torque:
+            w1, _, t1 = c1.run_with_torque(J, cb)
+            J2, cb2 = c2._torque_args(J, cb)
+            w2, _, t2 = c2.run_three_kernel(J2, cb2)
+            torch.cuda.synchronize()
+        else:
+            w1, _ = c1.run()
+            w2, _ = c2.run_three_kernel()
+            torch.cuda.synchronize()
+        for i, (a, b) in enumerate(zip(c1.former_inputs, c2.former_inputs)):
+            assert torch.equal(a, b), (step, "former input", i, (a - b).abs().max().item())
+        for i, (a, b) in enumerate(zip(c1.solution, c2.solution)):
+            assert torch.equal(a, b), (step, "solution", i, (a - b).abs().max().item())
+        assert torch.equal(w1, w2), step
+        if torque:
+            assert torch.equal(t1, t2), step
+        for name in ("world_position_desired", "yaw_desired", "first_run"):
+            assert torch.equal(getattr(c1, name), getattr(c2, name)), (step, name)
+
+
+@pytest.mark.gpu
+def test_one_launch_step_writes_only_the_wrench():
+    """keep_solution False (default): the step's solution buffers are left untouched."""
+    N, B = 10, 32
+    st, cmd, ctrl, params, gait_args, table = random_robot(B, 51, N, gait=True)
+    c = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    for t in c.buffers.outputs:
+        t.fill_(7.0)
+    w, _ = c.run()
+    torch.cuda.synchronize()
+    assert c.solution is None and torch.isfinite(w).all()
+    assert all(bool((t == 7.0).all()) for t in c.buffers.outputs)
+
+
+@pytest.mark.gpu
+def test_graphed_step_refuses_stale_or_converted_tensors():
+    from biped_pympc_amd.controller import GraphedMPCStep
+    N, B = 10, 16
+    st, cmd, ctrl, params, gait_args, table = random_robot(B, 61, N, gait=False)
+    c = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
+    c.state_estimate_data.root_position = c.state_estimate_data.root_position.double()
+    with pytest.raises(ValueError, match="root_position"):
+        GraphedMPCStep(c)
+    c.state_estimate_data.root_position = c.state_estimate_data.root_position.float()
+    g = GraphedMPCStep(c)
+    g()
+    c.set_contact_table(torch.from_numpy(table))  # replaces a captured tensor
+    with pytest.raises(RuntimeError, match="replaced"):
+        g()

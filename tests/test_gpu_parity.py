@@ -341,3 +341,51 @@ def test_golden_fixtures_on_the_hip_path(N):
                 e = rel_err_rows(out[k].cpu().numpy(), ref)
                 assert e.max() <= tol, (K, name, e.max())
         np.testing.assert_allclose(fused[5].cpu().numpy(), g[f"K{K}_mu"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("N", [10, 20, 5])
+@pytest.mark.parametrize("K,tol", [(1, 1e-10), (10, 1e-7)])
+def test_ccs_entry_from_arbitrary_x_init(N, K, tol):
+    """srbd_pdipm_ccs: the reference's _ccs solver init (sparse_pdipm_solver.py:30-35 and
+    initialize_pdipm_variables :537-558, restated in numpy here exactly as the reference writes
+    it: s = max(h - G x_init, 1), z = 1, y = 0) followed by K iterations, vs the oracle."""
+    B = 48
+    wl = make_workload(B, N, seed=700 + N + K, random_gait=True)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    dims = layout.Dims(N)
+    x0 = np.random.default_rng(N + K).normal(0, 5.0, (B, dims.nz))
+    Gd = layout.to_dense(G, *layout.ccs_G(N), (dims.n_ineq, dims.nz))
+    s0 = np.maximum(d - np.einsum("bij,bj->bi", Gd, x0), 1.0)
+    it = [x0, s0, np.ones((B, dims.n_ineq)), np.zeros((B, dims.n_eq))]
+    ref = oracle.pdipm(N, K, [H, G, A, f, d, b, *it])
+    out = solver.pdipm_ccs(_cuda([H, G, A, f, d, b]), _cuda([x0])[0], N, K)
+    torch.cuda.synchronize()
+    # y starts at 0 here, and after one iteration it is the first dual step of the delta-regularised
+    # equality rows: the two CPU restatements (sparse LDL^T oracle, dense LU) already disagree by up
+    # to 1.2e-9 (N = 10) / 7.8e-9 (N = 5) on these envs (scripts/ccs_floor.py), so y gets 3e-8 at K = 1
+    for k in range(4):
+        e = rel_err_rows(out[k].cpu().numpy(), ref[k])
+        assert e.max() <= (max(tol, 3e-8) if k == 3 else tol), (k, e.max())
+    assert np.all(np.isfinite(out[5].cpu().numpy()))
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_fused_step_qp_vectors_only_on_request(N):
+    """srbd_mpc_solve_fused keeps f, b, d on chip by default; keep_qp writes them, equal to the
+    former's own rows, and the solution is the same either way."""
+    B = 37
+    wl = make_workload(B, N, seed=800 + N, random_gait=True)
+    ins = _cuda(wl.inputs)
+    qp = solver.qp_former(ins, N)
+    bufs = solver.MPCSolveBuffers.allocate(N, B, "cuda")
+    bufs.workspace.fill_(3.0)
+    a = [t.clone() for t in solver.mpc_solve(ins, N, 10, buffers=bufs)]
+    torch.cuda.synchronize()
+    assert bool((bufs.workspace == 3.0).all())
+    c = solver.mpc_solve(ins, N, 10, buffers=bufs, keep_qp=True)
+    torch.cuda.synchronize()
+    for x, y in zip(a, c):
+        assert torch.equal(x, y)
+    views = bufs.qp_views()
+    for k in (1, 3, 5):  # f, b, d
+        assert torch.equal(views[k], qp[k]), k

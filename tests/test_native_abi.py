@@ -33,8 +33,8 @@ def _exports(path):
 def test_header_declares_the_cusadi_symbol_and_extended_api():
     names = _declared_functions()
     assert "evaluate" in names
-    assert {"srbd_qp_former", "srbd_pdipm", "srbd_pdipm_cold", "srbd_mpc_solve",
-            "srbd_last_error", "srbd_abi_version"} <= names
+    assert {"srbd_qp_former", "srbd_pdipm", "srbd_pdipm_cold", "srbd_pdipm_ccs", "srbd_mpc_solve",
+            "srbd_mpc_solve_fused", "srbd_mpc_step", "srbd_last_error", "srbd_abi_version"} <= names
 
 
 def test_core_library_exports_every_declared_symbol():
@@ -83,3 +83,12 @@ def test_bad_arguments_return_errors_without_touching_the_gpu():
     assert L.srbd_qp_former(10, 0, nulls, nulls, None) == 0
     assert L.srbd_pdipm(10, 5, 0, nulls, nulls, None) == 0
     assert L.srbd_pdipm_cold(10, 5, 0, 1.0, nulls, nulls, None) == 0
+    assert L.srbd_pdipm_ccs(10, 5, 4, nulls, nulls, None) != 0
+    assert "x_init" in _native.last_error()
+    # the one-launch controller step: N = 10 / 20 only, prep required
+    prep = _native.MPCPrep()
+    assert L.srbd_mpc_step(15, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
+    assert "horizon 10 or 20" in _native.last_error()
+    assert L.srbd_mpc_step(10, 20, 4, 1.0, None, None, None, None, 0, None, None, None, None) != 0
+    assert L.srbd_mpc_step(10, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
+    assert L.srbd_mpc_step(10, 20, 0, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) == 0

@@ -47,6 +47,21 @@ def _oracle_solve(local_inputs):
     return torch.from_numpy(x)
 
 
+class _PersistentSolve:
+    """The oracle solve writing into ONE preallocated buffer, as the HIP path's MPCSolveBuffers do:
+    a result handed out by reference would be overwritten by the next step."""
+
+    def __init__(self):
+        self.buf = None
+
+    def __call__(self, local_inputs):
+        x = _oracle_solve(local_inputs)
+        if self.buf is None:
+            self.buf = torch.empty_like(x)
+        self.buf.copy_(x)
+        return self.buf
+
+
 def _rank_main(rank, world, port, total, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -56,8 +71,13 @@ def _rank_main(rank, world, port, total, out_path):
         sh = ShardedMPC(N, K, total, device="cpu", solve_fn=_oracle_solve)
         u0 = sh.step(sh.local_slice(glob)).clone()
         u0b = sh.step(sh.local_slice(glob)).clone()  # buffers reused across steps
-        hs = [sh.step_async(sh.local_slice(glob)) for _ in range(3)]  # gathers left in flight
-        u0c = [h.wait().clone() for h in hs]
+        # three DIFFERENT steps with their gathers left in flight, results read only at the end and
+        # not copied: each handle must own its u0 (send / receive pairs and the solve buffer reused)
+        sha = ShardedMPC(N, K, total, device="cpu", solve_fn=_PersistentSolve())
+        globs = [[torch.from_numpy(a) for a in make_workload(total, N, seed=3000 + k, random_gait=True).inputs]
+                 for k in range(3)]
+        hs = [sha.step_async(sha.local_slice(g)) for g in globs]
+        u0c = [h.wait() for h in hs]
         if rank == 0:
             np.save(out_path, np.stack([u0.numpy(), u0b.numpy()] + [u.numpy() for u in u0c]))
     finally:
@@ -75,11 +95,20 @@ def test_gloo_world2_gather_equals_single_process(tmp_path, total):
     out = str(tmp_path / "u0.npy")
     mp.spawn(_rank_main, args=(2, _free_port(), total, out), nprocs=2, join=True)
     got = np.load(out)
-    wl = make_workload(total, N, seed=2024, random_gait=True)
-    ref = _oracle_solve([torch.from_numpy(a) for a in wl.inputs]).numpy()[:, 12 * N:12 * N + 12]
+    refs = [_oracle_solve([torch.from_numpy(a) for a in make_workload(total, N, seed=sd, random_gait=True).inputs]
+                          ).numpy()[:, 12 * N:12 * N + 12] for sd in (2024, 2024, 3000, 3001, 3002)]
     assert got.shape == (5, total, 12)
     for k in range(5):
-        assert np.array_equal(got[k], ref), k
+        assert np.array_equal(got[k], refs[k]), k
+
+
+def test_step_async_single_process_results_are_owned():
+    """world 1: step_async's handle must not alias the solve buffer the next step overwrites."""
+    sh = ShardedMPC(N, K, 4, device="cpu", solve_fn=_PersistentSolve())
+    globs = [[torch.from_numpy(a) for a in make_workload(4, N, seed=50 + k).inputs] for k in range(3)]
+    hs = [sh.step_async(g) for g in globs]
+    for g, h in zip(globs, hs):
+        assert torch.equal(h.wait(), _oracle_solve(g)[:, 12 * N:12 * N + 12])
 
 
 def test_single_process_path_without_process_group():
