@@ -1350,7 +1350,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     PROF_ADD_CTX(C, 5);
     C.template solve<1>(sigma * mu * 1.0);  // (spelling the phases out here costs N = 20 spills)
     // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
-    // K = 10 / 20 parity where no refinement has it (profiles/r02/refinement_parity.txt)
+    // K = 10 / 20 parity where no refinement has it, only the first 3 / 5 / 7 lets the degenerate
+    // duals of K = 20 drift to 2e-5 (profiles/r02/refinement_parity.txt, refinement_variants.txt)
     C.refine_rhs();
     C.template solve_chain<false>();
     C.template solve_finish<true>();
