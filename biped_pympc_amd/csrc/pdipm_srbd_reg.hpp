@@ -795,14 +795,17 @@ struct RegCtx {
         VV[q] = di[t] * (r2 + wd[t] * rs[t]);
       }
     }
+    // The x columns and the scalar u columns of t = Phi^-1 r1~ do not depend on the complementarity
+    // right-hand side, and the affine solve_finish (kAffine) leaves them in TV: the combined solve
+    // (kMode 1) recomputes only the foot columns.
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
       const int c = lane + TPB * t;
-      if (c < nx) TV[c] = -rxx[t] * IX[c % 12];
+      if (kMode == 0 && c < nx) TV[c] = -rxx[t] * IX[c % 12];
     }
     __syncthreads();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
-    if (lane < 3 * N) {
+    if (lane < (kMode == 0 ? 3 : 2) * N) {
       if (lane < 2 * N) {
         const int i = lane >> 1, f = lane & 1, b = 12 * i;
         double rv[4];
@@ -934,8 +937,11 @@ struct RegCtx {
 
   // kRefine: the refinement step -- TV holds dx and QV the dual correction c, so the same updates
   // give dx - Phi~^-1 A^T c; the x-moment duals move by their 2x2 formula's increment, and dz, ds are
-  // re-formed from the refined dx (with the combined solve's VV, r_s)
-  template <bool kRefine = false>
+  // re-formed from the refined dx (with the combined solve's VV, r_s).
+  // kAffine: the affine (predictor) direction, of which only ds and dz are consumed (step lengths,
+  // mu_aff and the corrector's ds o dz, sparse_pdipm_solver.py:484-490): G touches only the foot
+  // columns, so dx is finished on those alone (no x columns, no scalar columns, no x-moment duals).
+  template <bool kRefine = false, bool kAffine = false>
   SRBD_PHASE_ATTR __device__ void solve_finish() {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
@@ -944,15 +950,15 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int c = lane + TPB * t;
-      if (c < nx) {
+      if (!kAffine && c < nx) {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         if (k < N) aty += mcol(Mc, j, QV + 12 * k);
         TV[c] = TV[c] - aty * IX[j];
       }
     }
-    if (lane < 3 * N) {
-      const bool foot = lane < 2 * N;
+    if (lane < (kAffine ? 2 : 3) * N) {
+      const bool foot = kAffine || lane < 2 * N;
       const int i = foot ? (lane >> 1) : lane - 2 * N;
       const int b = nx + 12 * i;
       const double* yi = QV + 12 * i;
@@ -1336,7 +1342,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.template solve_rhs<0>(0.0);
     C.template factor_chain<true>();  // + the affine forward elimination
     C.template solve_chain<true>();
-    C.solve_finish();
+    C.template solve_finish<false, true>();
     const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
     double sza = 0.0;
     ul = C.fresh_lane();
