@@ -186,21 +186,40 @@ __device__ __forceinline__ void v_rows(double (&V)[12], const double (&Dr)[12], 
 struct CoupleRow {
   double d, b, a0, a1, a2;
 };
-__device__ __forceinline__ double couple_cw(const CoupleRow& c, double w) {
-  double acc = c.d * w + c.b * shl6(w);
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%1", "%2", 6) SRBD_FMAC_BC("%0", "%1", "%3", 7)
-      SRBD_FMAC_BC("%0", "%1", "%4", 8) "s_nop 1\n"
-      : "+v"(acc)
+// Both with two accumulators (short dependent paths); the forward form folds the subtraction from
+// the right-hand side into its first FMA: base - C w, and C^T y.
+__device__ __forceinline__ double couple_cw_sub(const CoupleRow& c, double w, double base) {
+  double a1 = fma(-c.d, w, base);
+  double a2 = -c.b * shl6(w);
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "-%3", 6) SRBD_FMAC_BC("%1", "%2", "-%4", 7)
+      SRBD_FMAC_BC("%0", "%2", "-%5", 8) "s_nop 1\n"
+      : "+v"(a1), "+v"(a2)
       : "v"(w), "v"(c.a0), "v"(c.a1), "v"(c.a2));
-  return acc;
+  return a1 + a2;
 }
-__device__ __forceinline__ double couple_cty(const CoupleRow& c, double y) {
-  double acc = c.d * y + c.b * shr6(y);
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%1", "%2", 0) SRBD_FMAC_BC("%0", "%1", "%3", 1)
-      SRBD_FMAC_BC("%0", "%1", "%4", 2) "s_nop 1\n"
-      : "+v"(acc)
+__device__ __forceinline__ double couple_cty2(const CoupleRow& c, double y) {
+  double a1 = c.d * y;
+  double a2 = c.b * shr6(y);
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", 0) SRBD_FMAC_BC("%1", "%2", "%4", 1)
+      SRBD_FMAC_BC("%0", "%2", "%5", 2) "s_nop 1\n"
+      : "+v"(a1), "+v"(a2)
       : "v"(y), "v"(c.a0), "v"(c.a1), "v"(c.a2));
-  return acc;
+  return a1 + a2;
+}
+// init - sum_j c[j] v(lane j) over the 12 rows of a 16-lane DPP row: two accumulators (the
+// broadcast-FMAs issue every 8 cycles, so each accumulator's FMAs are 16 cycles apart) and one add
+__device__ __forceinline__ double dot_bc12_sub(const double (&c)[12], double v, double init) {
+  double a0 = init, a1 = 0.0;
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%2", "-%3", 0) SRBD_FMAC_BC("%1", "%2", "-%4", 1) SRBD_FMAC_BC("%0", "%2", "-%5", 2)
+      SRBD_FMAC_BC("%1", "%2", "-%6", 3) SRBD_FMAC_BC("%0", "%2", "-%7", 4) SRBD_FMAC_BC("%1", "%2", "-%8", 5)
+      SRBD_FMAC_BC("%0", "%2", "-%9", 6) SRBD_FMAC_BC("%1", "%2", "-%10", 7) SRBD_FMAC_BC("%0", "%2", "-%11", 8)
+      SRBD_FMAC_BC("%1", "%2", "-%12", 9) SRBD_FMAC_BC("%0", "%2", "-%13", 10) SRBD_FMAC_BC("%1", "%2", "-%14", 11)
+      "s_nop 1\n"
+      : "+v"(a0), "+v"(a1)
+      : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
+        "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));
+  return a0 + a1;
 }
 
 // element (c, b) of a compact M / C block (c or b runtime)
@@ -447,6 +466,18 @@ struct RegCtx {
     return block_sum(sz) / m;
   }
 
+  // Right-hand side of forward elimination step t: g_i - C w_{i-1} (base = this lane's g_i entry),
+  // and at the middle step also - C^T v_{mid+1} of group 1 (its lanes compute - C v with base 0
+  // and hand it to group 0 through ds_bpermute)
+  __device__ static double fwd_rhs(bool act, bool prev, bool mstep, int g, int r, const CoupleRow& Cr, double w,
+                                   const double* qv) {
+    double q = 0.0;
+    if (act && !(mstep && g == 1)) q = *qv;
+    if (act && prev) q = couple_cw_sub(Cr, w, q);
+    if (mstep && nb >= 1) q += __shfl(q, 16 + perm12(r), 64);  // group 0 += group 1's - C^T v_{mid+1}
+    return q;
+  }
+
   // -------------------------------------------------------------------- factorise ----
   __device__ void factor() {
     factor_build();
@@ -664,12 +695,8 @@ struct RegCtx {
           for (int c = 0; c < 12; ++c) dv_at(DV, offs[c], imm) = Dr[c];
         }
         if constexpr (kFwd) {  // the solve chain's forward step t (solve_chain), Dr = D_i^-1 row
-          double cw = 0.0;
-          if (act && prev) cw = couple_cw(Cr, wf);
-          double mv = 0.0;
-          if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
+          const double q = fwd_rhs(act, prev, mstep, g, r, Cr, wf, QV + 12 * i + pr);
           if (act && !(mstep && g == 1)) {
-            const double q = (QV[12 * i + pr] - cw) - mv;
             wf = dot_bc12(Dr, q);
             if (own) QV[12 * i + pr] = wf;
           }
@@ -894,16 +921,12 @@ struct RegCtx {
         const int i = mstep ? mid : (g ? N - 1 - t : t);
         const bool act = mstep ? true : (t < cnt);
         const bool prev = mstep ? (cnt >= 1) : (t >= 1);
-        double cw = 0.0;
-        if (act && prev) cw = couple_cw(Cr, w);
-        double mv = 0.0;
-        if (mstep && nb >= 1) mv = __shfl(cw, 16 + perm12(r), 64);  // group 1's C^T v_{mid+1}
+        const double q = fwd_rhs(act, prev, mstep, g, r, Cr, w, QV + 12 * i + pr);
         if (act && !(mstep && g == 1)) {
           const int imm = mstep ? kDvBytes * (N - 1) : 2 * kDvBytes * t;
           double Dr[12];
 #pragma unroll
           for (int k = 0; k < 12; ++k) Dr[k] = dv_at(DV, offs[k], imm);
-          const double q = (QV[12 * i + pr] - cw) - mv;
           w = dot_bc12(Dr, q);
 #pragma unroll
           for (int k = 0; k <= T; ++k) wv[k] = (k == t) ? w : wv[k];
@@ -925,8 +948,7 @@ struct RegCtx {
           double Dr[12];
 #pragma unroll
           for (int k = 0; k < 12; ++k) Dr[k] = dv_at(DV, offs[k], 2 * kDvBytes * te);
-          const double sc = couple_cty(Ct, y);  // Cg^T y_prev
-          y = wv[te] - dot_bc12(Dr, sc);
+          y = dot_bc12_sub(Dr, couple_cty2(Ct, y), wv[te]);  // w_te - D^-1 Cg^T y_prev
           if (own) QV[12 * i + pr] = y;
         }
       }
