@@ -398,7 +398,9 @@ struct RegCtx {
       QV[q.e] = v + re[t];
     }
   }
-  SRBD_PHASE_ATTR __device__ double residuals() {
+  // want_mu (wave-uniform): also return mu = s^T z / m -- the first iteration only: afterwards it
+  // equals the previous iteration's mu_new, the same products s_t z_t summed in the same order
+  SRBD_PHASE_ATTR __device__ double residuals(bool want_mu) {
     const int lane = fresh_lane();
     const double *X = at(Lo::X), *Y = at(Lo::Y), *Z = at(Lo::Z), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd),
                  *Gf = at(Lo::Gf), *Pd = at(Lo::Pd), *Hu = at(Lo::Hu), *SG = at(Lo::SG);
@@ -463,7 +465,7 @@ struct RegCtx {
       }
     }
     __syncthreads();
-    return block_sum(sz) / m;
+    return want_mu ? block_sum(sz) / m : 0.0;
   }
 
   // Right-hand side of forward elimination step t: g_i - C w_{i-1} (base = this lane's g_i entry),
@@ -1342,7 +1344,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
-    const double mu = C.residuals();
+    double mu = C.residuals(it == 0);
+    if (it > 0) mu = mu_new;
     int ul = C.fresh_lane();
     if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)
       double a = 0.0, b = 0.0, c = 0.0;

@@ -261,12 +261,14 @@ __device__ __forceinline__ double rcp3(double d) {
 // DPP tree in the VALU (no LDS round trips): quads, half-rows, rows through quad_perm / mirrors,
 // then row_bcast:15 / row_bcast:31 fold the four 16-lane rows into lane 63, read back uniformly.
 // Rows left out by a row_mask see `id`, the operation's identity. All 64 lanes must be active.
+// The first four levels read a valid lane everywhere, so they are plain DPP moves (no old value to
+// materialise first: two v_mov_b32 fewer per level).
 template <class Op>
 __device__ __forceinline__ double wave_reduce(double v, double id, Op op) {
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xF, 0xF, false));  // row_mirror
+  v = op(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));  // row_half_mirror
+  v = op(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));  // row_mirror
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xA, 0xF, false));  // row_bcast:15 -> rows 1, 3
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xC, 0xF, false));  // row_bcast:31 -> rows 2, 3
   const long long b = __double_as_longlong(v);
