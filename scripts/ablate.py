@@ -107,8 +107,20 @@ VARIANTS = {
     # one extra back-substitution pass over the refinement's QV (a chain's cost; results change)
     "chain2": lambda s: s.replace("    C.refine_rhs();\n    C.template solve_chain<false>();",
                                   "    C.refine_rhs();\n    C.template solve_chain<false>();\n    C.template solve_chain<true>();"),
-    "residuals2": lambda s: s.replace("    const double mu = C.residuals();",
-                                      "    (void)C.residuals();\n    const double mu = C.residuals();"),
+    "residuals2": lambda s: s.replace("    double mu = C.residuals(it == 0);",
+                                      "    (void)C.residuals(false);\n    double mu = C.residuals(it == 0);"),
+    # the factor chain with the fused affine forward elimination run twice (not idempotent: the
+    # second pass inverts the inverses; cost only)
+    "fchain2": lambda s: s.replace("    C.template factor_chain<true>();  // + the affine forward elimination",
+                                   "    C.template factor_chain<true>();\n    C.template factor_chain<true>();"),
+    # the combined solve's right-hand side twice (idempotent)
+    "rhs2": lambda s: s.replace("    solve_rhs<kMode>(smu);\n    solve_chain<false>();",
+                                "    solve_rhs<kMode>(smu);\n    solve_rhs<kMode>(smu);\n    solve_chain<false>();"),
+    # the combined solve's finish twice (cost only)
+    "finish2": lambda s: s.replace("    solve_chain<false>();\n    solve_finish<false>();",
+                                   "    solve_chain<false>();\n    solve_finish<false>();\n    solve_finish<false>();"),
+    # the refinement's residual (KKT rows 1, 4) twice (cost only)
+    "refine2": lambda s: s.replace("    C.refine_rhs();\n", "    C.refine_rhs();\n    C.refine_rhs();\n"),
 }
 
 
