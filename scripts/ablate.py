@@ -119,6 +119,17 @@ VARIANTS = {
     # the combined solve's finish twice (cost only)
     "finish2": lambda s: s.replace("    solve_chain<false>();\n    solve_finish<false>();",
                                    "    solve_chain<false>();\n    solve_finish<false>();\n    solve_finish<false>();"),
+    # odd workgroups start their Newton loop ~40k cycles late (5 x s_sleep 127), so the two waves
+    # sharing a SIMD tend to sit in different phases (chain vs row-parallel) -- a phase-offset probe
+    "stagger": lambda s: s.replace("  PROF_MARK_CTX(C);\n",
+                                   "  PROF_MARK_CTX(C);\n  if (blockIdx.x & 1) {\n"
+                                   "    for (int k = 0; k < 5; ++k) __builtin_amdgcn_s_sleep(127);\n  }\n"),
+    # the same without the progress-ordered wave priority (which pulls the two waves back together)
+    "stagger_noprio": lambda s: s.replace("  PROF_MARK_CTX(C);\n",
+                                          "  PROF_MARK_CTX(C);\n  if (blockIdx.x & 1) {\n"
+                                          "    for (int k = 0; k < 5; ++k) __builtin_amdgcn_s_sleep(127);\n  }\n")
+                                 .replace("#define SRBD_PROGRESS_PRIO 1", "#define SRBD_PROGRESS_PRIO 0"),
+    "noprio": lambda s: s.replace("#define SRBD_PROGRESS_PRIO 1", "#define SRBD_PROGRESS_PRIO 0"),
     # the refinement's residual (KKT rows 1, 4) twice (cost only)
     "refine2": lambda s: s.replace("    C.refine_rhs();\n", "    C.refine_rhs();\n    C.refine_rhs();\n"),
 }
