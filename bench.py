@@ -317,6 +317,8 @@ def main():
                        "pdipm_iters": K, "qp_dims": [d.nz, d.n_eq, d.n_ineq],
                        "parallelism": f"dp{world}" + (f" (u0 all_gather over {'RCCL' if backend == 'nccl' else backend})"
                                                       if world > 1 else "")},
+            # solves/s without the u0 gather (every rank's shard solve alone), N > 1 only
+            "value_without_gather": (round(world * B / (ms_main * 1e-3), 1) if dist is not None else None),
             "kernels_ms": {"mpc_step_fused": round(ms_fused, 4) if fused else None,
                            "qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
                            "u0_all_gather": None if ms_gather is None else round(ms_gather, 4)},
