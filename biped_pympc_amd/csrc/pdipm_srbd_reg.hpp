@@ -1102,10 +1102,12 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     // ---- the stage blocks from the former inputs (qp_former.hpp's former_model) ----
     FormerLds& F = *reinterpret_cast<FormerLds*>(smem + Lo::TV);  // TV..DYm are free until the solve
     static_assert(sizeof(FormerLds) <= sizeof(double) * (Lo::total - Lo::TV), "former scratch fits");
+    // The 17 former inputs of this env live in DV (dead until the first factor) for the whole
+    // prologue: prepared there (controller step) or staged there from memory in one round trip
+    static_assert(4 * 12 * N + 2 * N + 44 <= 80 * N, "former inputs fit the DV blocks");
     const double* P[17];
-    if (fa.ctrl) {  // controller step: the inputs are prepared here, into DV (dead until the first factor)
-      static_assert(4 * 12 * N + 2 * N + 44 <= 80 * N, "former inputs fit the DV blocks");
-      double* o[17];
+    double* o[17];
+    {
       int off = 0;
 #pragma unroll
       for (int i = 0; i < 17; ++i) {
@@ -1113,6 +1115,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         P[i] = o[i];
         off += former_in_nnz(i, N);
       }
+    }
+    if (fa.ctrl) {  // controller step: the inputs are prepared here
       if (lane < 64) prepare_env(fa.prep, env, lane, o);
       __syncthreads();
       if (fa.prep.out[0]) {  // the caller also wants the prepared inputs in memory
@@ -1123,9 +1127,30 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
           for (int e = lane; e < w; e += TPB) g[e] = o[i][e];
         }
       }
-    } else {
+    } else {  // every load issued before any store: one memory round trip instead of the former
+              // model's chain of dependent global reads (measured 60k cycles of prologue per QP)
+      static_assert(12 * N <= 2 * TPB, "every former input row fits two passes of the QP's threads");
+      double v[17][2];
 #pragma unroll
-      for (int i = 0; i < 17; ++i) P[i] = fa.in[i] + (size_t)env * former_in_nnz(i, N);
+      for (int i = 0; i < 17; ++i) {
+        const int w = former_in_nnz(i, N);
+        const double* g = fa.in[i] + (size_t)env * w;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int e = lane + TPB * t;
+          v[i][t] = (TPB * t < w && e < w) ? g[e] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 17; ++i) {
+        const int w = former_in_nnz(i, N);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int e = lane + TPB * t;
+          if (TPB * t < w && e < w) o[i][e] = v[i][t];
+        }
+      }
+      __syncthreads();
     }
     former_model(F, P, lane);
     const double mu = P[6][0];
