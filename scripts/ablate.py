@@ -130,6 +130,12 @@ VARIANTS = {
                                           "    for (int k = 0; k < 5; ++k) __builtin_amdgcn_s_sleep(127);\n  }\n")
                                  .replace("#define SRBD_PROGRESS_PRIO 1", "#define SRBD_PROGRESS_PRIO 0"),
     "noprio": lambda s: s.replace("#define SRBD_PROGRESS_PRIO 1", "#define SRBD_PROGRESS_PRIO 0"),
+    # the S_ii build's sparse-entry stage loop fully unrolled (the product unrolls it by 2)
+    "sii_unroll": lambda s: s.replace("#pragma unroll 2\n      for (int i = wv * (N / NW);",
+                                      "#pragma unroll\n      for (int i = wv * (N / NW);"),
+    # the Phi_u foot-block inverses with rcp3 pivots instead of IEEE division
+    "foot_rcp": lambda s: s.replace("      sweep_inverse<4>(a);  // IEEE pivots",
+                                    "      sweep_inverse<4, true>(a);  // IEEE pivots"),
     # the refinement's residual (KKT rows 1, 4) twice (cost only)
     "refine2": lambda s: s.replace("    C.refine_rhs();\n", "    C.refine_rhs();\n    C.refine_rhs();\n"),
 }
