@@ -374,6 +374,11 @@ struct RegCtx {
     return v;
   }
   __device__ double block_sum(double v) { return block_reduce<false>(v); }
+  // the QP's threads vote (wave-uniform result)
+  __device__ bool block_any(bool p) {
+    if constexpr (TPB == 64) return __any(p);
+    else return block_reduce<true>(p ? 0.0 : 1.0) < 0.5;
+  }
   __device__ double block_min(double v) { return block_reduce<true>(v); }
   // The lane index, re-materialised as an opaque value at the start of every phase: keeps the
   // compiler from hoisting each phase's per-lane addresses and predicates out of the Newton loop
@@ -724,8 +729,8 @@ struct RegCtx {
   // dz, ds). The affine solve's forward elimination runs inside factor_chain<true> instead, with
   // each block's inverse still in registers (solve_chain<true> then only substitutes back).
   template <int kMode>
-  __device__ void solve(double smu) {
-    solve_rhs<kMode>(smu);
+  __device__ void solve(double smu, bool rx = false) {
+    solve_rhs<kMode>(smu, rx);
     solve_chain<false>();
     solve_finish<false>();
   }
@@ -737,20 +742,26 @@ struct RegCtx {
   // symmetric inverse), so dy is off by ~eps cond |dy| and dx_u = Phi_u^-1 (r - N^T dy) multiplies
   // that by 1e4: 1e-7 relative in x after one iteration against the oracle's sparse LDL^T; and as
   // the barrier sharpens (W = z / s -> 1e8) the reduced foot rows r~ = -r_x - G^T D^-1 (r2 - W r3)
-  // cancel against Phi_f dx_f. Rows 2 and 3 hold by construction (ds, dz are formed from them);
-  // the correction K [cx; cy] = [e1; e4] is taken block Gauss-Seidel, which is the same elimination
-  // (cx = Phi^-1 (e1 - A^T cy), S cy = A Phi^-1 e1 - e4):
-  //   1. dx_f += Phi_f^-1 e1_f on the foot columns, e1 = -r_x - (H + beta) dx - G^T dz - A^T dy
-  //      (the other columns' Phi is diagonal and their row-1 residual is rounding only);
-  //   2. rho = A_dyn dx + r_e - delta dy, KKT row 4's residual = the dual residual g - S dy
-  //      (the x-moment rows are eliminated exactly by their 2x2 blocks);
+  // cancel against Phi_f dx_f. At degenerate iterates (s and z both at their 1e-8 clamps, Lambda
+  // ~ 4e7, cond Phi_f ~ 4e12) rows 2 and 3 -- which ds, dz are formed from -- lose digits too: a
+  // correction from rows 1 and 4 alone then stalls at ~1e-6 in dx while one from all four rows
+  // reaches ~1e-11 (CPU emulation of this elimination, scripts/dual_refine_emu_stress.py;
+  // profiles/r02/refinement_4row.txt). The correction K c = e of all four residuals,
+  //   e1 = -r_x - (H + beta) dx - G^T dz - A^T dy   (foot columns: the other columns' Phi is
+  //        diagonal with no G, so their row-1 residual is rounding only)
+  //   e2 = r2 - (W ds + dz),   e3 = -r_s - (G dx + ds - delta dz),   e4 = -r_e - (A dx - delta dy)
+  // is taken through the same elimination, block Gauss-Seidel:
+  //   0. q = D^-1 (e2 - W e3) per inequality row; VV += q and r_s -= e3, so that solve_finish<true>'s
+  //      re-formation dz = VV + Lambda G dx, ds = -r_s - G dx + delta dz yields dz + c_z, ds + c_s;
+  //   1. dx_f += Phi_f^-1 (e1 - G^T q) on the foot columns (G^T (dz + q) in one pass over Z);
+  //   2. rho = A_dyn dx + r_e - delta dy = A t_c - e4 (the x-moment rows are eliminated exactly by
+  //      their 2x2 blocks);
   //   3. one more chain solve S c = rho; dy += c, dx -= Phi~^-1 A^T c (solve_finish<true>, which
   //      leaves row 1 as step 1 made it) and dz, ds re-formed from dx.
-  // This sits at the dense-LU-vs-oracle floor over 512 envs per case at K = 1/10/20 (the full
-  // residual of both rows with a second right-hand-side solve measures the same and costs 6 % more
-  // on the fused step: profiles/r02/refinement_variants.txt). dy is parked in RXu (r_x's u part is
-  // dead once step 1 has read it) while QV carries rho and then c.
-  template <int t>
+  // On the SURVEY workloads this sits at the dense-LU-vs-oracle floor over 512 envs per case at
+  // K = 1/10/20 (profiles/r02/refinement_variants.txt). dy is parked in RXu (r_x's u part is dead
+  // once step 1 has read it) while QV carries rho and then c.
+  template <int t, bool kPark>
   __device__ void rho_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV,
                            double* DYs) {
     const ERow q = erow(fresh_lane(), t);
@@ -759,18 +770,36 @@ struct RegCtx {
       v += Pd[q.r] * TV[12 * q.i + q.r];
       v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
       const double dy = QV[q.e];  // read and rewritten by its owner lane only
-      DYs[q.e] = dy;
+      if (kPark) DYs[q.e] = dy;
       QV[q.e] = (v + re[t]) - kDelta * dy;
     }
   }
+  // kAff: the affine (predictor) direction at a degenerate iterate (see the main loop): r_s stays
+  // (the combined solve needs it), e3 goes to Z for solve_finish<true, true>, and dy is not parked
+  // (RXu still feeds the combined solve)
+  template <bool kAff = false>
   SRBD_PHASE_ATTR __device__ void refine_rhs() {
     const int lane = fresh_lane();
     const double *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
     double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z);
+    double* VV = at(Lo::VV);
+    double e3r[SI];
 #pragma unroll
-    for (int t = 0; t < SI; ++t) {  // dz to LDS for G^T dz (Z's z mirror is dead until the update)
+    for (int t = 0; t < SI; ++t) {  // step 0 (owner regs); dz + q to LDS for G^T (dz + q) (Z's z mirror
+                                    // is dead until the update)
       const int q = lane + TPB * t;
-      if (q < m) Zd[q] = dz[t];
+      e3r[t] = 0.0;
+      if (q < m) {
+        const int i = q / 16, k = q % 16;
+        const double gd = grow4(Gf, k, TV + nx + 12 * i);
+        const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
+        const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
+        const double qc = di[t] * (e2 - wd[t] * e3);
+        VV[q] = VV[q] + qc;
+        if (kAff) e3r[t] = e3;
+        else rs[t] = rs[t] - e3;
+        Zd[q] = dz[t] + qc;
+      }
     }
     __syncthreads();
     if (lane < 2 * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
@@ -810,16 +839,23 @@ struct RegCtx {
       }
     }
     __syncthreads();
-    rho_slot<0>(TV, Mc, Pd, Nd, QV, DYs);
-    rho_slot<1>(TV, Mc, Pd, Nd, QV, DYs);
+    if (kAff) {  // Z is dead from here on: it keeps e3 for solve_finish<true, true>
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (lane + TPB * t < m) Zd[lane + TPB * t] = e3r[t];
+    }
+    rho_slot<0, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
+    rho_slot<1, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
     __syncthreads();
     PROF_ADD(6);
   }
 
+  // rx (combined solve only): recompute the x / scalar columns of t -- the affine direction was
+  // refined, so its full finish overwrote them in TV
   template <int kMode>
-  SRBD_PHASE_ATTR __device__ void solve_rhs(double smu) {
+  SRBD_PHASE_ATTR __device__ void solve_rhs(double smu, bool rx = false) {
     const int lane = fresh_lane();
-    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV);
+    double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *Zr2 = at(Lo::Z);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
                  *SG = at(Lo::SG), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd);
 #pragma unroll
@@ -829,6 +865,7 @@ struct RegCtx {
         const double si = rcp3(s[t]);
         double r2 = -(si * (s[t] * z[t]));
         if (kMode == 1) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
+        Zr2[q] = r2;  // row 2's right-hand side for refine_rhs (Z is dead until the update)
         VV[q] = di[t] * (r2 + wd[t] * rs[t]);
       }
     }
@@ -838,11 +875,11 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
       const int c = lane + TPB * t;
-      if (kMode == 0 && c < nx) TV[c] = -rxx[t] * IX[c % 12];
+      if ((kMode == 0 || rx) && c < nx) TV[c] = -rxx[t] * IX[c % 12];
     }
     __syncthreads();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
-    if (lane < (kMode == 0 ? 3 : 2) * N) {
+    if (lane < ((kMode == 0 || rx) ? 3 : 2) * N) {
       if (lane < 2 * N) {
         const int i = lane >> 1, f = lane & 1, b = 12 * i;
         double rv[4];
@@ -1034,7 +1071,9 @@ struct RegCtx {
         const int i = q / 16, k = q % 16;
         const double gd = grow4(Gf, k, TV + nx + 12 * i);
         dz[t] = VV[q] + di[t] * wd[t] * gd;
-        ds[t] = -rs[t] - gd + kDelta * dz[t];
+        // the affine refinement keeps r_s and parks its row-3 residual e3 in Z (refine_rhs<true>)
+        const double r3 = (kRefine && kAffine) ? at(Lo::Z)[q] - rs[t] : -rs[t];
+        ds[t] = r3 - gd + kDelta * dz[t];
       }
     }
     PROF_ADD(3);
@@ -1379,6 +1418,19 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
+    // A degenerate iterate -- some s at its 1e-8 clamp (sparse_pdipm_solver.py:520) -- has rows
+    // with W = z / s up to ~1e8, where the reduced solve's affine ds, dz lose most digits; its error
+    // then enters sigma and the corrector (profiles/r02/refinement_4row.txt). Such iterations also
+    // refine the affine direction (the QP is one wave or two joined ones: a uniform branch).
+    bool degen;
+    {
+      const int l = C.fresh_lane();
+      bool p = false;
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (l + TPB * t < m) p = p || (C.s[t] <= 1e-8);
+      degen = C.block_any(p);
+    }
     int ul = C.fresh_lane();
     if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)
       double a = 0.0, b = 0.0, c = 0.0;
@@ -1400,7 +1452,14 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.template solve_rhs<0>(0.0);
     C.template factor_chain<true>();  // + the affine forward elimination
     C.template solve_chain<true>();
-    C.template solve_finish<false, true>();
+    if (degen) {  // full affine finish (rho needs all of dx), then the 4-row refinement
+      C.template solve_finish<false, false>();
+      C.template refine_rhs<true>();
+      C.template solve_chain<false>();
+      C.template solve_finish<true, true>();
+    } else {
+      C.template solve_finish<false, true>();
+    }
     const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
     double sza = 0.0;
     ul = C.fresh_lane();
@@ -1412,7 +1471,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
     __syncthreads();
     PROF_ADD_CTX(C, 5);
-    C.template solve<1>(sigma * mu * 1.0);  // (spelling the phases out here costs N = 20 spills)
+    C.template solve<1>(sigma * mu * 1.0, degen);  // (spelling the phases out here costs N = 20 spills)
     // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
     // K = 10 / 20 parity where no refinement has it, only the first 3 / 5 / 7 lets the degenerate
     // duals of K = 20 drift to 2e-5 (profiles/r02/refinement_parity.txt, refinement_variants.txt)

@@ -79,11 +79,15 @@ class Workload:
 
 def make_workload(B: int, N: int = 10, seed: int = 0, random_gait: bool = False,
                   residuals: bool = False, contact_layout: str = "reference",
-                  dt: float = DT_MPC) -> Workload:
+                  dt: float = DT_MPC, tilt: float = 0.15, residual_scale: float = 0.5,
+                  contact_override: np.ndarray | None = None) -> Workload:
+    """SURVEY 8d synthetic robots. Stress knobs (defaults = the SURVEY distributions): ``tilt`` bounds
+    roll and pitch, ``residual_scale`` is the std of the RL residual accelerations (with
+    ``residuals``), ``contact_override`` (B, N, 2) replaces the contact schedule (e.g. flight)."""
     rng = np.random.default_rng(seed)
     d = Dims(N)
-    roll = rng.uniform(-0.15, 0.15, B)
-    pitch = rng.uniform(-0.15, 0.15, B)
+    roll = rng.uniform(-tilt, tilt, B)
+    pitch = rng.uniform(-tilt, tilt, B)
     yaw = rng.uniform(-math.pi, math.pi, B)
     R = rot_zyx(roll, pitch, yaw)
     Iw = R @ HECTOR_I_BODY[None] @ np.swapaxes(R, 1, 2)
@@ -117,14 +121,16 @@ def make_workload(B: int, N: int = 10, seed: int = 0, random_gait: bool = False,
     else:
         contact = np.ones((B, N, 2), np.int32)
         ssp = dsp = phase = None
+    if contact_override is not None:
+        contact = np.asarray(contact_override, np.int32).reshape(B, N, 2)
     if contact_layout == "reference":
         ct_flat = contact.reshape(B, 2 * N).astype(np.float64)  # row-major, as the caller does
     elif contact_layout == "casadi":
         ct_flat = np.swapaxes(contact, 1, 2).reshape(B, 2 * N).astype(np.float64)
     else:
         raise ValueError(contact_layout)
-    a_lin = rng.normal(0.0, 0.5, (B, 3)) if residuals else np.zeros((B, 3))
-    a_ang = rng.normal(0.0, 0.5, (B, 3)) if residuals else np.zeros((B, 3))
+    a_lin = rng.normal(0.0, residual_scale, (B, 3)) if residuals else np.zeros((B, 3))
+    a_ang = rng.normal(0.0, residual_scale, (B, 3)) if residuals else np.zeros((B, 3))
     inputs = [
         x0,
         np.ones((B, 12 * N)),

@@ -136,6 +136,8 @@ VARIANTS = {
     # the Phi_u foot-block inverses with rcp3 pivots instead of IEEE division
     "foot_rcp": lambda s: s.replace("      sweep_inverse<4>(a);  // IEEE pivots",
                                     "      sweep_inverse<4, true>(a);  // IEEE pivots"),
+    # no affine refinement at degenerate iterates (the branch compiled out)
+    "no_aff_ref": lambda s: s.replace("    if (degen) {  // full affine finish", "    if (false) {  // full affine finish"),
     # the refinement's residual (KKT rows 1, 4) twice (cost only)
     "refine2": lambda s: s.replace("    C.refine_rhs();\n", "    C.refine_rhs();\n    C.refine_rhs();\n"),
 }
