@@ -353,6 +353,7 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
+  double e3r[SI];  // the affine refinement's row-3 residuals (degenerate iterations only)
   PROF_DECL
 
   __device__ double* at(int off) const { return L + off; }
@@ -732,7 +733,7 @@ struct RegCtx {
   __device__ void solve(double smu, bool rx = false) {
     solve_rhs<kMode>(smu, rx);
     solve_chain<false>();
-    solve_finish<false>();
+    solve_finish<false, false, true>();
   }
 
   // One step of iterative refinement of the combined direction d = (dx, ds, dz, dy) against the
@@ -782,26 +783,25 @@ struct RegCtx {
     const int lane = fresh_lane();
     const double *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
     double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z);
-    double* VV = at(Lo::VV);
-    double e3r[SI];
+    if constexpr (kAff) {  // step 0 for the affine direction (the combined one ran it in its finish)
+      double *VV = at(Lo::VV);
 #pragma unroll
-    for (int t = 0; t < SI; ++t) {  // step 0 (owner regs); dz + q to LDS for G^T (dz + q) (Z's z mirror
-                                    // is dead until the update)
-      const int q = lane + TPB * t;
-      e3r[t] = 0.0;
-      if (q < m) {
-        const int i = q / 16, k = q % 16;
-        const double gd = grow4(Gf, k, TV + nx + 12 * i);
-        const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
-        const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
-        const double qc = di[t] * (e2 - wd[t] * e3);
-        VV[q] = VV[q] + qc;
-        if (kAff) e3r[t] = e3;
-        else rs[t] = rs[t] - e3;
-        Zd[q] = dz[t] + qc;
+      for (int t = 0; t < SI; ++t) {
+        const int q = lane + TPB * t;
+        e3r[t] = 0.0;
+        if (q < m) {
+          const int i = q / 16, k = q % 16;
+          const double gd = grow4(Gf, k, TV + nx + 12 * i);
+          const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
+          const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
+          const double qc = di[t] * (e2 - wd[t] * e3);
+          VV[q] = VV[q] + qc;
+          e3r[t] = e3;
+          Zd[q] = dz[t] + qc;
+        }
       }
     }
-    __syncthreads();
+    __syncthreads();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
     if (lane < 2 * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
       const int i = lane >> 1, f = lane & 1, b = 12 * i;
       const double* zf = Zd + 16 * i + 8 * f;
@@ -1010,7 +1010,10 @@ struct RegCtx {
   // kAffine: the affine (predictor) direction, of which only ds and dz are consumed (step lengths,
   // mu_aff and the corrector's ds o dz, sparse_pdipm_solver.py:484-490): G touches only the foot
   // columns, so dx is finished on those alone (no x columns, no scalar columns, no x-moment duals).
-  template <bool kRefine = false, bool kAffine = false>
+  // kStep0: refine_rhs's step 0 for the combined direction fused into the row loop, where dz, ds,
+  // G dx and VV are at hand -- e2, e3, q = D^-1 (e2 - W e3); VV += q, Z = dz + q for G^T (dz + q),
+  // r_s -= e3
+  template <bool kRefine = false, bool kAffine = false, bool kStep0 = false>
   SRBD_PHASE_ATTR __device__ void solve_finish() {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
@@ -1070,10 +1073,20 @@ struct RegCtx {
       if (q < m) {
         const int i = q / 16, k = q % 16;
         const double gd = grow4(Gf, k, TV + nx + 12 * i);
-        dz[t] = VV[q] + di[t] * wd[t] * gd;
+        const double vq = VV[q];
+        dz[t] = vq + di[t] * wd[t] * gd;
         // the affine refinement keeps r_s and parks its row-3 residual e3 in Z (refine_rhs<true>)
         const double r3 = (kRefine && kAffine) ? at(Lo::Z)[q] - rs[t] : -rs[t];
         ds[t] = r3 - gd + kDelta * dz[t];
+        if constexpr (kStep0) {
+          double* Zd = at(Lo::Z);
+          const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
+          const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
+          const double qc = di[t] * (e2 - wd[t] * e3);
+          VV[q] = vq + qc;
+          rs[t] = rs[t] - e3;
+          Zd[q] = dz[t] + qc;
+        }
       }
     }
     PROF_ADD(3);
