@@ -1107,6 +1107,33 @@ struct RegCtx {
     mn = block_min(mn);
     return fmax(fmin(1.0, 0.99 * mn), 1e-12);
   }
+  __device__ double step_min(const double (&v)[SI], const double (&dv)[SI]) {
+    const int lane = fresh_lane();
+    double mn = INFINITY;
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {
+      const int q = lane + TPB * t;
+      if (q < m) {
+        const bool c = dv[t] < 0.0;
+        const double a = -v[t] * rcp3(dv[t]);
+        mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
+      }
+    }
+    return mn;
+  }
+  // The primal and dual step lengths: at one wave per QP their two min-reductions run as one
+  // interleaved DPP tree (the same values as two step_length calls)
+  __device__ void step_lengths(double& ap, double& ad) {
+    if constexpr (TPB == 64) {
+      double mp = step_min(s, ds), md = step_min(z, dz);
+      wave_min2(mp, md);
+      ap = fmax(fmin(1.0, 0.99 * mp), 1e-12);
+      ad = fmax(fmin(1.0, 0.99 * md), 1e-12);
+    } else {
+      ap = step_length(s, ds);
+      ad = step_length(z, dz);
+    }
+  }
 };
 
 // Arguments of the fused former + solver kernel (srbd_mpc_solve_fused): the 17 qp_former inputs
@@ -1473,7 +1500,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     } else {
       C.template solve_finish<false, true>();
     }
-    const double ap = C.step_length(C.s, C.ds), ad = C.step_length(C.z, C.dz);
+    double ap, ad;
+    C.step_lengths(ap, ad);
     double sza = 0.0;
     ul = C.fresh_lane();
 #pragma unroll
@@ -1491,7 +1519,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.refine_rhs();
     C.template solve_chain<false>();
     C.template solve_finish<true>();
-    const double apc = C.step_length(C.s, C.ds), adc = C.step_length(C.z, C.dz);
+    double apc, adc;
+    C.step_lengths(apc, adc);
     __syncthreads();
     double szn = 0.0;
     ul = C.fresh_lane();

@@ -275,6 +275,32 @@ __device__ __forceinline__ double wave_reduce(double v, double id, Op op) {
   const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// Two independent reductions as one interleaved tree: each level's DPP moves and ops of the two
+// values are independent, so the second hides the first's DPP -> VALU latency (same results as two
+// wave_reduce calls, level by level).
+template <class Op>
+__device__ __forceinline__ void wave_reduce2(double& a, double& b, double id, Op op) {
+  a = op(a, __builtin_amdgcn_mov_dpp(a, 0xB1, 0xF, 0xF, true));
+  b = op(b, __builtin_amdgcn_mov_dpp(b, 0xB1, 0xF, 0xF, true));
+  a = op(a, __builtin_amdgcn_mov_dpp(a, 0x4E, 0xF, 0xF, true));
+  b = op(b, __builtin_amdgcn_mov_dpp(b, 0x4E, 0xF, 0xF, true));
+  a = op(a, __builtin_amdgcn_mov_dpp(a, 0x141, 0xF, 0xF, true));
+  b = op(b, __builtin_amdgcn_mov_dpp(b, 0x141, 0xF, 0xF, true));
+  a = op(a, __builtin_amdgcn_mov_dpp(a, 0x140, 0xF, 0xF, true));
+  b = op(b, __builtin_amdgcn_mov_dpp(b, 0x140, 0xF, 0xF, true));
+  a = op(a, __builtin_amdgcn_update_dpp(id, a, 0x142, 0xA, 0xF, false));
+  b = op(b, __builtin_amdgcn_update_dpp(id, b, 0x142, 0xA, 0xF, false));
+  a = op(a, __builtin_amdgcn_update_dpp(id, a, 0x143, 0xC, 0xF, false));
+  b = op(b, __builtin_amdgcn_update_dpp(id, b, 0x143, 0xC, 0xF, false));
+  const long long ba = __double_as_longlong(a), bb = __double_as_longlong(b);
+  const int alo = __builtin_amdgcn_readlane((int)ba, 63), ahi = __builtin_amdgcn_readlane((int)(ba >> 32), 63);
+  const int blo = __builtin_amdgcn_readlane((int)bb, 63), bhi = __builtin_amdgcn_readlane((int)(bb >> 32), 63);
+  a = __longlong_as_double(((long long)ahi << 32) | (unsigned int)alo);
+  b = __longlong_as_double(((long long)bhi << 32) | (unsigned int)blo);
+}
+__device__ inline void wave_min2(double& a, double& b) {
+  wave_reduce2(a, b, INFINITY, [](double x, double y) { return fmin(x, y); });
+}
 __device__ inline double wave_sum(double v) {
   return wave_reduce(v, 0.0, [](double a, double b) { return a + b; });
 }
