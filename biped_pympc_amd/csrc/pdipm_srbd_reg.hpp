@@ -35,6 +35,23 @@ namespace srbd {
 // chains and the per-stage tasks stay on wave 0.
 __host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : 128; }
 
+// Ordering of LDS accesses between the threads of one QP. A two-wave QP (N = 20) needs the
+// workgroup barrier. A one-wave QP needs no wait at all: LDS operations of one wavefront are
+// performed in order (AMDGPU memory model: s_waitcnt lgkmcnt(0) synchronises LDS between
+// wavefronts of a workgroup, not within one), so a wavefront-scope fence -- a code-motion barrier
+// that emits no s_waitcnt -- orders a phase's LDS writes before the next phase's reads. (A
+// one-wave __syncthreads drains every outstanding LDS operation at each phase boundary.)
+template <int TPB>
+__device__ __forceinline__ void qp_sync() {
+  if constexpr (TPB > 64) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 template <int N, int TPB = reg_tpb(N)>
 struct RegLayout {
   static constexpr int nz = 24 * N, m = 16 * N, p = 14 * N, nx = 12 * N;
@@ -369,7 +386,7 @@ struct RegCtx {
       double* R = at(Lo::RED) + 2 * red_k;
       red_k ^= 1;
       if ((lane & 63) == 0) R[lane >> 6] = v;
-      __syncthreads();
+      qp_sync<TPB>();
       v = kMin ? fmin(R[0], R[1]) : R[0] + R[1];
     }
     return v;
@@ -478,7 +495,7 @@ struct RegCtx {
         sz += s[t] * z[t];
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     return want_mu ? block_sum(sz) / m : 0.0;
   }
 
@@ -515,7 +532,7 @@ struct RegCtx {
         VV[q] = di[t] * wd[t];  // Lambda, shared with the foot tasks
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     if (lane < 2 * N) {  // foot blocks of Phi_u, inverted; kept in this lane's registers
       const int i = lane >> 1, f = lane & 1;
       double a[10];
@@ -544,7 +561,7 @@ struct RegCtx {
         PHs[20 * i + 10 * f + e] = a[e];
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in two divergence-free passes over the class-sorted entry
     // table (TRI = c_tab.dvo: 21 dense x dense entries, then 57 with a sparse index): an entry
     // touching rows {3,4,5,9,10,11} of N needs 10 FMAs instead of 40
@@ -619,7 +636,7 @@ struct RegCtx {
         DV[kDvStride * dv_pos<N>(i) + sl] = v;
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD(1);
   }
 
@@ -719,7 +736,7 @@ struct RegCtx {
         }
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD(2);
   }
 
@@ -801,7 +818,7 @@ struct RegCtx {
         }
       }
     }
-    __syncthreads();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
+    qp_sync<TPB>();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
     if (lane < 2 * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
       const int i = lane >> 1, f = lane & 1, b = 12 * i;
       const double* zf = Zd + 16 * i + 8 * f;
@@ -838,7 +855,7 @@ struct RegCtx {
         TV[nx + b + foot_colj(f, a)] += t;
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     if (kAff) {  // Z is dead from here on: it keeps e3 for solve_finish<true, true>
 #pragma unroll
       for (int t = 0; t < SI; ++t)
@@ -846,7 +863,7 @@ struct RegCtx {
     }
     rho_slot<0, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
     rho_slot<1, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD(6);
   }
 
@@ -877,7 +894,7 @@ struct RegCtx {
       const int c = lane + TPB * t;
       if ((kMode == 0 || rx) && c < nx) TV[c] = -rxx[t] * IX[c % 12];
     }
-    __syncthreads();
+    qp_sync<TPB>();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
     if (lane < ((kMode == 0 || rx) ? 3 : 2) * N) {
       if (lane < 2 * N) {
@@ -919,10 +936,10 @@ struct RegCtx {
         TV[nx + b + 11] = -RXu[b + 11] * SG[3];
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
     g_slot<1>(TV, Mc, Pd, Nd, QV);
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD(3);
   }
 
@@ -1000,7 +1017,7 @@ struct RegCtx {
         }
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD(4);
   }
 
@@ -1066,7 +1083,7 @@ struct RegCtx {
         }
       }
     }
-    __syncthreads();
+    qp_sync<TPB>();
 #pragma unroll
     for (int t = 0; t < SI; ++t) {  // dz, ds (owner regs)
       const int q = lane + TPB * t;
@@ -1197,7 +1214,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     if (fa.ctrl) {  // controller step: the inputs are prepared here
       if (lane < 64) prepare_env(fa.prep, env, lane, o);
-      __syncthreads();
+      qp_sync<TPB>();
       if (fa.prep.out[0]) {  // the caller also wants the prepared inputs in memory
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
@@ -1229,7 +1246,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
           if (TPB * t < w && e < w) o[i][e] = v[i][t];
         }
       }
-      __syncthreads();
+      qp_sync<TPB>();
     }
     former_model(F, P, lane);
     const double mu = P[6][0];
@@ -1249,7 +1266,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       e6 = F.UB[c_tab.e6];
       e9 = F.UB[c_tab.e9];
     }
-    __syncthreads();
+    qp_sync<TPB>();
     if (lane < 28) Gf[g_row(c_tab.grow[lane]) + foot_pos(c_tab.gcol[lane])] = former_g(lane, mu);
     // f, b, h straight into the registers of the lanes that use them (load_qp_vectors' mapping);
     // the rows reach memory only if the caller asked for them
@@ -1315,7 +1332,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       e6 = Ag[a_ubase(N) + c_tab.e6];
       e9 = Ag[a_ubase(N) + c_tab.e9];
     }
-    __syncthreads();
+    qp_sync<TPB>();
     if (lane < 28) Gf[g_row(c_tab.grow[lane]) + foot_pos(c_tab.gcol[lane])] = Gg[lane];
     // ---- stage-invariance check (bitwise): every periodic block equals the first one ----
     // x_k blocks (36 values, k = 1..N-1) vs x_1's; the x_N single entries vs x_1's +I entries (P);
@@ -1333,9 +1350,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     bad = __any(bad);
     if constexpr (TPB > 64) {  // one verdict for the whole QP (both waves leave or both stay)
       if ((lane & 63) == 0) reinterpret_cast<int*>(smem + Lo::RED)[lane >> 6] = bad;
-      __syncthreads();
+      qp_sync<TPB>();
       bad = reinterpret_cast<int*>(smem + Lo::RED)[0] | reinterpret_cast<int*>(smem + Lo::RED)[1];
-      __syncthreads();  // RED is reused by the first block reduction
+      qp_sync<TPB>();  // RED is reused by the first block reduction
     }
     if (bad) {
       if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
@@ -1358,7 +1375,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     SG[8] = 1.0 / (p6 * kDelta + e6 * e6);
     SG[9] = 1.0 / (p9 * kDelta + e9 * e9);
   }
-  __syncthreads();
+  qp_sync<TPB>();
   if (lane < 24) {  // compact M and C (C = M diag(P / phi_x)); group 1's block is pi C^T pi^T
     int r, j;
     if (lane < 12) { r = lane; j = lane; }
@@ -1390,12 +1407,12 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   // ---- iterate ----
   // X aliases the dense M the K0 / K1 loop above reads: with two waves, the other wave must be past
   // that loop before X is written (one wave runs both loops in order)
-  if constexpr (TPB > 64) __syncthreads();
+  if constexpr (TPB > 64) qp_sync<TPB>();
   double *X = smem + Lo::X, *Z = smem + Lo::Z, *Y = smem + Lo::Y;
   if (!kFused && args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     for (int e = lane; e < nz; e += TPB) X[e] = xg[e];
-    __syncthreads();
+    qp_sync<TPB>();
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
@@ -1435,7 +1452,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     for (int e = lane; e < p; e += TPB) Y[e] = kFused ? fa.y0 : args.y0;
   }
-  __syncthreads();
+  qp_sync<TPB>();
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
   const double* TV = smem + Lo::TV;
@@ -1510,7 +1527,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double mu_aff = C.block_sum(sza) / m;
     const double ratio = mu_aff / mu;
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD_CTX(C, 5);
     C.template solve<1>(sigma * mu * 1.0, degen);  // (spelling the phases out here costs N = 20 spills)
     // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
@@ -1521,7 +1538,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.template solve_finish<true>();
     double apc, adc;
     C.step_lengths(apc, adc);
-    __syncthreads();
+    qp_sync<TPB>();
     double szn = 0.0;
     ul = C.fresh_lane();
     for (int e = ul; e < nz; e += TPB) X[e] = X[e] + apc * TV[e];
@@ -1543,7 +1560,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       Y[e] = Y[e] + adc * dye;
     }
     mu_new = C.block_sum(szn) / m;
-    __syncthreads();
+    qp_sync<TPB>();
     PROF_ADD_CTX(C, 5);
   }
   PROF_FLUSH(C);
@@ -1586,7 +1603,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         wl[lane] = w;
       }
       if (fa.tau) {
-        __syncthreads();
+        qp_sync<TPB>();
         const int nd = fa.ndof;
         for (int q = lane; q < 2 * nd; q += TPB) {
           const int l = q / nd, k = q - l * nd;
