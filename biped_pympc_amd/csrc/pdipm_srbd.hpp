@@ -67,8 +67,16 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
 // v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
 // they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
-// entry (VALU write -> DPP read needs 2 wait states) and on exit (a compiler DPP may read what the
-// block wrote). Inside a block no instruction reads a register an earlier one in the block wrote.
+// entry (VALU write -> DPP read needs 2 wait states). Inside a block no instruction reads a
+// register an earlier one in the block wrote.
+// No wait states at the END of a block: a DPP the compiler emits after a block gets its own from
+// the hazard recognizer (it treats the block's outputs as VALU writes), and every block starts with
+// its own s_nop 1 for the DPP inside it. Dropping the trailing s_nop 1 of every block (231 per N=10
+// step kernel) was bit-identical and 1.5 % (N = 10) / 2.0 % (N = 20) faster;
+// -DSRBD_ASM_TAIL='"s_nop 1\n"' restores it (A/B switch).
+#ifndef SRBD_ASM_TAIL
+#define SRBD_ASM_TAIL ""
+#endif
 #define SRBD_FMAC_BC(D, S, C, K) "v_fmac_f64_dpp " D ", " S ", " C " row_newbcast:" #K " row_mask:0xf bank_mask:0xf\n"
 
 // one Gauss-Jordan pivot update: S[j] -= S[j](lane K) * t for the 11 columns j != K (the caller
@@ -79,7 +87,7 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
   SRBD_FMAC_BC("%6", "%6", "-%11", K) SRBD_FMAC_BC("%7", "%7", "-%11", K) SRBD_FMAC_BC("%8", "%8", "-%11", K) \
   SRBD_FMAC_BC("%9", "%9", "-%11", K) SRBD_FMAC_BC("%10", "%10", "-%11", K)
 #define SRBD_PIVOT11(K, a, b, c, d, e, f, g, h, i, j, l)                                             \
-  asm("s_nop 1\n" SRBD_FMAC11(K) "s_nop 1\n"                                                        \
+  asm("s_nop 1\n" SRBD_FMAC11(K) SRBD_ASM_TAIL                                                        \
       : "+v"(S[a]), "+v"(S[b]), "+v"(S[c]), "+v"(S[d]), "+v"(S[e]), "+v"(S[f]), "+v"(S[g]), "+v"(S[h]), \
         "+v"(S[i]), "+v"(S[j]), "+v"(S[l])                                                          \
       : "v"(t))
@@ -108,7 +116,7 @@ __device__ __forceinline__ double dot_bc12(const double (&c)[12], double v) {
       SRBD_FMAC_BC("%0", "%3", "%7", 3) SRBD_FMAC_BC("%1", "%3", "%8", 4) SRBD_FMAC_BC("%2", "%3", "%9", 5)
       SRBD_FMAC_BC("%0", "%3", "%10", 6) SRBD_FMAC_BC("%1", "%3", "%11", 7) SRBD_FMAC_BC("%2", "%3", "%12", 8)
       SRBD_FMAC_BC("%0", "%3", "%13", 9) SRBD_FMAC_BC("%1", "%3", "%14", 10) SRBD_FMAC_BC("%2", "%3", "%15", 11)
-      "s_nop 1\n"
+      SRBD_ASM_TAIL
       : "+v"(a0), "+v"(a1), "+v"(a2)
       : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
         "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));

@@ -153,7 +153,7 @@ __device__ __forceinline__ double shl6(double v) { return __builtin_amdgcn_mov_d
       SRBD_FMAC_BC("%3", "%7", N6, 6) SRBD_FMAC_BC("%0", "%4", N7, 7) SRBD_FMAC_BC("%1", "%5", N7, 7) \
       SRBD_FMAC_BC("%2", "%6", N7, 7) SRBD_FMAC_BC("%3", "%7", N7, 7) SRBD_FMAC_BC("%0", "%4", N8, 8) \
       SRBD_FMAC_BC("%1", "%5", N8, 8) SRBD_FMAC_BC("%2", "%6", N8, 8) SRBD_FMAC_BC("%3", "%7", N8, 8) \
-      "s_nop 1\n"                                                                                   \
+      SRBD_ASM_TAIL                                                                                   \
       : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)                                                      \
       : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c6), "v"(c7), "v"(c8))
 template <bool kNeg = false>
@@ -174,15 +174,15 @@ __device__ __forceinline__ double shr6(double v) { return __builtin_amdgcn_mov_d
 // holds C's row c as (d, a0, a1, a2, b)
 #define SRBD_VROW_A(C)                                                                              \
   asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C)               \
-      SRBD_FMAC_BC("%0", "%6", "%7", C) SRBD_FMAC_BC("%0", "%8", "%9", C) "s_nop 1\n"              \
+      SRBD_FMAC_BC("%0", "%6", "%7", C) SRBD_FMAC_BC("%0", "%8", "%9", C) SRBD_ASM_TAIL              \
       : "=&v"(V[C])                                                                                 \
       : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(a0), "v"(Dr[6]), "v"(a1), "v"(Dr[7]), "v"(a2), "v"(Dr[8]))
 #define SRBD_VROW_B(C)                                                                              \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C) "s_nop 1\n"  \
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C) SRBD_ASM_TAIL  \
       : "=&v"(V[C])                                                                                 \
       : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(b), "v"(Dr[C + 6]))
 #define SRBD_VROW_D(C)                                                                              \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) "s_nop 1\n" : "=&v"(V[C]) : "0"(0.0), "v"(d), "v"(Dr[C]))
+  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_ASM_TAIL : "=&v"(V[C]) : "0"(0.0), "v"(d), "v"(Dr[C]))
 __device__ __forceinline__ void v_rows(double (&V)[12], const double (&Dr)[12], double d, double a0, double a1,
                                        double a2, double b) {
   SRBD_VROW_A(0);
@@ -213,7 +213,7 @@ __device__ __forceinline__ double couple_cw_sub(const CoupleRow& c, double w, do
   double a1 = fma(-c.d, w, base);
   double a2 = -c.b * shl6(w);
   asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "-%3", 6) SRBD_FMAC_BC("%1", "%2", "-%4", 7)
-      SRBD_FMAC_BC("%0", "%2", "-%5", 8) "s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%2", "-%5", 8) SRBD_ASM_TAIL
       : "+v"(a1), "+v"(a2)
       : "v"(w), "v"(c.a0), "v"(c.a1), "v"(c.a2));
   return a1 + a2;
@@ -222,7 +222,7 @@ __device__ __forceinline__ double couple_cty2(const CoupleRow& c, double y) {
   double a1 = c.d * y;
   double a2 = c.b * shr6(y);
   asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", 0) SRBD_FMAC_BC("%1", "%2", "%4", 1)
-      SRBD_FMAC_BC("%0", "%2", "%5", 2) "s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%2", "%5", 2) SRBD_ASM_TAIL
       : "+v"(a1), "+v"(a2)
       : "v"(y), "v"(c.a0), "v"(c.a1), "v"(c.a2));
   return a1 + a2;
@@ -236,7 +236,7 @@ __device__ __forceinline__ double dot_bc12_sub(const double (&c)[12], double v, 
       SRBD_FMAC_BC("%1", "%2", "-%6", 3) SRBD_FMAC_BC("%0", "%2", "-%7", 4) SRBD_FMAC_BC("%1", "%2", "-%8", 5)
       SRBD_FMAC_BC("%0", "%2", "-%9", 6) SRBD_FMAC_BC("%1", "%2", "-%10", 7) SRBD_FMAC_BC("%0", "%2", "-%11", 8)
       SRBD_FMAC_BC("%1", "%2", "-%12", 9) SRBD_FMAC_BC("%0", "%2", "-%13", 10) SRBD_FMAC_BC("%1", "%2", "-%14", 11)
-      "s_nop 1\n"
+      SRBD_ASM_TAIL
       : "+v"(a0), "+v"(a1)
       : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
         "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]));
