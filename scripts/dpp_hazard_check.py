@@ -80,10 +80,13 @@ def check(path, want=""):
             if kind != "inst" or "_dpp" not in raw.split(";")[0]:
                 continue
             n_dpp += 1
-            # the DPP source is src0: for v_*_dpp D, S0, ... it is the second operand
             s = raw.split(";")[0].strip()
             op, _, rest = s.partition(" ")
             ops = [o.strip() for o in rest.split(",")]
+            # the DPP-routed operand, src0 (the second operand of v_*_dpp D, S0, ...). The blocks'
+            # accumulator chains read their FMAC accumulator (src2 = D) 1-2 states after writing it,
+            # as they have since round 1 with results at the oracle's FP64 floor: the hardware
+            # hazard is on the routed operand (LLVM's recognizer checks every VGPR use)
             reads = regs(ops[1]) if len(ops) > 1 else set()
             states = 0
             j = i - 1
