@@ -172,31 +172,34 @@ __device__ __forceinline__ double shr6(double v) { return __builtin_amdgcn_mov_d
 // V = D^-1 C^T row by row: V[c] = Dr[c] C[c][c] + (c < 3: sum_k Dr[6 + k] C[c][6 + k])
 // + (3 <= c < 6: Dr[c + 6] C[c][c + 6]), the coefficients of row c broadcast from lane c, which
 // holds C's row c as (d, a0, a1, a2, b)
-#define SRBD_VROW_A(C)                                                                              \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C)               \
-      SRBD_FMAC_BC("%0", "%6", "%7", C) SRBD_FMAC_BC("%0", "%8", "%9", C) SRBD_ASM_TAIL              \
-      : "=&v"(V[C])                                                                                 \
-      : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(a0), "v"(Dr[6]), "v"(a1), "v"(Dr[7]), "v"(a2), "v"(Dr[8]))
-#define SRBD_VROW_B(C)                                                                              \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_FMAC_BC("%0", "%4", "%5", C) SRBD_ASM_TAIL  \
-      : "=&v"(V[C])                                                                                 \
-      : "0"(0.0), "v"(d), "v"(Dr[C]), "v"(b), "v"(Dr[C + 6]))
-#define SRBD_VROW_D(C)                                                                              \
-  asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", C) SRBD_ASM_TAIL : "=&v"(V[C]) : "0"(0.0), "v"(d), "v"(Dr[C]))
+// Three blocks (rows 0..2, 3..5, 6..11) rather than one per row: the accumulator chains of a
+// block's rows interleave (each FMA's accumulator was written 2-5 instructions earlier, not by the
+// previous one), and two leading s_nop instead of eleven
 __device__ __forceinline__ void v_rows(double (&V)[12], const double (&Dr)[12], double d, double a0, double a1,
                                        double a2, double b) {
-  SRBD_VROW_A(0);
-  SRBD_VROW_A(1);
-  SRBD_VROW_A(2);
-  SRBD_VROW_B(3);
-  SRBD_VROW_B(4);
-  SRBD_VROW_B(5);
-  SRBD_VROW_D(6);
-  SRBD_VROW_D(7);
-  SRBD_VROW_D(8);
-  SRBD_VROW_D(9);
-  SRBD_VROW_D(10);
-  SRBD_VROW_D(11);
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%6", "%10", 0) SRBD_FMAC_BC("%1", "%6", "%11", 1) SRBD_FMAC_BC("%2", "%6", "%12", 2)
+      SRBD_FMAC_BC("%0", "%7", "%13", 0) SRBD_FMAC_BC("%1", "%7", "%13", 1) SRBD_FMAC_BC("%2", "%7", "%13", 2)
+      SRBD_FMAC_BC("%0", "%8", "%14", 0) SRBD_FMAC_BC("%1", "%8", "%14", 1) SRBD_FMAC_BC("%2", "%8", "%14", 2)
+      SRBD_FMAC_BC("%0", "%9", "%15", 0) SRBD_FMAC_BC("%1", "%9", "%15", 1) SRBD_FMAC_BC("%2", "%9", "%15", 2)
+      SRBD_ASM_TAIL
+      : "=&v"(V[0]), "=&v"(V[1]), "=&v"(V[2])
+      : "0"(0.0), "1"(0.0), "2"(0.0), "v"(d), "v"(a0), "v"(a1), "v"(a2), "v"(Dr[0]), "v"(Dr[1]), "v"(Dr[2]),
+        "v"(Dr[6]), "v"(Dr[7]), "v"(Dr[8]));
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%6", "%8", 3) SRBD_FMAC_BC("%1", "%6", "%9", 4) SRBD_FMAC_BC("%2", "%6", "%10", 5)
+      SRBD_FMAC_BC("%0", "%7", "%11", 3) SRBD_FMAC_BC("%1", "%7", "%12", 4) SRBD_FMAC_BC("%2", "%7", "%13", 5)
+      SRBD_ASM_TAIL
+      : "=&v"(V[3]), "=&v"(V[4]), "=&v"(V[5])
+      : "0"(0.0), "1"(0.0), "2"(0.0), "v"(d), "v"(b), "v"(Dr[3]), "v"(Dr[4]), "v"(Dr[5]), "v"(Dr[9]),
+        "v"(Dr[10]), "v"(Dr[11]));
+  asm("s_nop 1\n"
+      SRBD_FMAC_BC("%0", "%12", "%13", 6) SRBD_FMAC_BC("%1", "%12", "%14", 7) SRBD_FMAC_BC("%2", "%12", "%15", 8)
+      SRBD_FMAC_BC("%3", "%12", "%16", 9) SRBD_FMAC_BC("%4", "%12", "%17", 10) SRBD_FMAC_BC("%5", "%12", "%18", 11)
+      SRBD_ASM_TAIL
+      : "=&v"(V[6]), "=&v"(V[7]), "=&v"(V[8]), "=&v"(V[9]), "=&v"(V[10]), "=&v"(V[11])
+      : "0"(0.0), "1"(0.0), "2"(0.0), "3"(0.0), "4"(0.0), "5"(0.0), "v"(d), "v"(Dr[6]), "v"(Dr[7]), "v"(Dr[8]),
+        "v"(Dr[9]), "v"(Dr[10]), "v"(Dr[11]));
 }
 
 // (C w)_r and (C^T y)_r of the compact stage coupling for one vector held one element per lane:
