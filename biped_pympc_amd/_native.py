@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_void_p, ctypes.c_int]
     L.srbd_set_solver_path.restype = ctypes.c_int
     L.srbd_set_solver_path.argtypes = [ctypes.c_int]
+    L.srbd_get_solver_path.restype = ctypes.c_int
+    L.srbd_get_solver_path.argtypes = []
     L.srbd_pattern_ccs.restype = ctypes.c_int
     L.srbd_pattern_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_int)]
@@ -107,21 +109,37 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed: {msg}")
 
 
+SOLVER_PATHS = {"auto": 0, "general": 1, "lds": 2}
+
+
+def current_solver_path() -> int:
+    """Solver path code in effect for the current HIP device (0 = auto)."""
+    return lib().srbd_get_solver_path()
+
+
 class solver_path:
     """Context manager selecting the solver kernels: "auto" (stage-invariant kernels -- the
     register-resident one at N = 10 and 20 -- plus the general fallback), "general" (general kernel only)
-    or "lds" (the LDS-resident stage-invariant kernel at every horizon). For the current HIP device;
-    for tests/benchmarks."""
+    or "lds" (the LDS-resident stage-invariant kernel at every horizon). For the HIP device current
+    on entry; on exit the previous path of that device is restored. For tests/benchmarks.
+    ``srbd_mpc_step`` (the one-launch controller step) ignores the path."""
 
     def __init__(self, path: str):
-        self.code = {"auto": 0, "general": 1, "lds": 2}[path]
+        self.code = SOLVER_PATHS[path]
+        self._prev = None
+        self._device = None
 
     def __enter__(self):
+        import torch
+        self._device = torch.cuda.current_device()
+        self._prev = current_solver_path()
         check(lib().srbd_set_solver_path(self.code), "srbd_set_solver_path")
         return self
 
     def __exit__(self, *exc):
-        lib().srbd_set_solver_path(0)
+        import torch
+        with torch.cuda.device(self._device):
+            check(lib().srbd_set_solver_path(self._prev), "srbd_set_solver_path")
 
 
 def last_error() -> str:

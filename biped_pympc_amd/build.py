@@ -73,6 +73,21 @@ def build_dropin(kind: str, N: int, K: int | None) -> str:
     return _build_dropin_lib(fn, N, K, core, False, False)
 
 
+# the two HIP translation units of libsrbd_mpc.so and their unit-specific flags: the N = 20 register
+# kernels in their own unit, scheduled with the register-pressure trackers (csrc/reg20.hpp)
+HIP_UNITS = {
+    "srbd_mpc.hip": ["-DSRBD_SPLIT_REG20"],
+    "srbd_reg20.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+}
+
+
+def unit_compile_cmd(unit: str, extra: list[str]) -> list[str]:
+    """hipcc command line of one translation unit exactly as the product build compiles it (the
+    ISA audit, tests/test_isa_hazards.py, appends --cuda-device-only -S to the same flags)."""
+    return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", *HIP_UNITS[unit], *extra,
+            os.path.join(CSRC, unit)]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     core = os.path.join(LIB_DIR, "libsrbd_mpc.so")
@@ -84,10 +99,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         # trackers (csrc/reg20.hpp), linked into the same library
         obj20 = os.path.join(LIB_DIR, "srbd_reg20.o")
         obj_main = os.path.join(LIB_DIR, "srbd_mpc.o")
-        cmds = [[HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
-                 "-mllvm", "-amdgpu-use-amdgpu-trackers=1", "-o", obj20, os.path.join(CSRC, "srbd_reg20.hip")],
-                [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", "-DSRBD_SPLIT_REG20",
-                 "-o", obj_main, os.path.join(CSRC, "srbd_mpc.hip")],
+        cmds = [unit_compile_cmd("srbd_reg20.hip", ["-fPIC", "-c", "-o", obj20]),
+                unit_compile_cmd("srbd_mpc.hip", ["-fPIC", "-c", "-o", obj_main]),
                 [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", core, obj_main, obj20]]
         for cmd in cmds:
             if verbose:

@@ -282,7 +282,7 @@ class MPCControllerHIP(BaseMPCController):
         N, B = self.horizon_length, self.num_envs
         self.prepare()
         out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
-        self.solution = out
+        self.solution = out if self.cfg.keep_solution else None  # as run(): exposed on request only
         rot = _f32(self.state_estimate_data.rotation_body, self.device)
         rc = _native.lib().srbd_u0_wrench_torque(
             N, B, out[0].data_ptr(), rot.data_ptr(), self.foot_wrench.data_ptr(), 0 if J is None else J.shape[3],
@@ -328,8 +328,13 @@ class GraphedMPCStep:
 
     The graph records device pointers, so the state / command / schedule tensors must be contiguous
     float32 on the controller's device at capture (checked) and be updated IN PLACE (``copy_``)
-    between replays. A setter that replaces a tensor (set_state_estimate_data, set_contact_table,
-    set_gait, set_mpc_sampling_time, ...) invalidates the graph: the next replay raises.
+    between replays. Every replay first compares the storage of every source tensor -- the state
+    estimate and command fields, the contact schedule, dt_mpc, the residual accelerations, the
+    knot-point state -- with what was captured, and the constants baked into the graph (mass, mu,
+    I_body, Q, R, step dt, layout, iterations, y0): a tensor replaced by assignment
+    (``data.root_position = ...``, ``c.residual_lin_accel = x.clone()``, a setter) or a changed
+    constant makes the replay raise instead of silently reading the captured values. (Q and R given
+    as device tensors are compared by storage, not value.)
     """
 
     def __init__(self, controller: MPCControllerHIP, warmup: int = 1):
@@ -337,6 +342,7 @@ class GraphedMPCStep:
         self._keep: list = []
         self._prep = self.c._prep_struct(self._keep, strict=True)  # resolves every input pointer once
         self._version = controller._version
+        self._signature = self._current_signature()
         saved = [t.clone() for t in (controller.world_position_desired, controller.yaw_desired,
                                      controller.first_run)]
         s = torch.cuda.Stream()
@@ -362,14 +368,44 @@ class GraphedMPCStep:
                                             _native.ptr_array([t.data_ptr() for t in c.former_inputs]),
                                             solver._stream_ptr()), "srbd_prepare_inputs")
         out = solver.mpc_solve(c.former_inputs, N, c.cfg.pdipm_iterations, c.cfg.y0, c.buffers)
-        c.solution = out
+        c.solution = out if c.cfg.keep_solution else None
         _native.check(L.srbd_u0_wrench(N, c.num_envs, out[0].data_ptr(), self._prep.rotation_body,
                                        c.foot_wrench.data_ptr(), solver._stream_ptr()), "srbd_u0_wrench")
+
+    def _current_signature(self) -> tuple:
+        """(name, storage pointer) of every tensor the step reads or updates, plus the constants the
+        graph bakes in -- without converting or synchronising anything."""
+        c, st, ds = self.c, self.c.state_estimate_data, self.c.desired_state_data
+        src = [(n, getattr(st, n)) for n in ("root_euler", "root_position", "root_angular_velocity_w",
+                                             "root_velocity_w", "rotation_body", "foot_position")]
+        src += [(n, getattr(ds, n)) for n in ("desired_velocity_b", "desired_angular_velocity_b", "desired_height")]
+        src += [(n, getattr(c, n)) for n in ("world_position_desired", "yaw_desired", "first_run", "dt_mpc",
+                                             "residual_lin_accel", "residual_ang_accel")]
+        if c._gait is not None:
+            src += list(zip(("gait_phase", "ssp_durations", "dsp_durations"), c._gait))
+        else:
+            src.append(("contact_table", c.contact_table))
+
+        def value(v):
+            if isinstance(v, torch.Tensor):
+                return ("device", v.data_ptr()) if v.is_cuda else tuple(v.reshape(-1).tolist())
+            return tuple(v) if isinstance(v, (list, tuple)) else v
+        consts = (("mass", c.mass), ("mu", c.mu), ("I_body", value(c.I_body)), ("Q", value(c.Q)),
+                  ("R", value(c.R)), ("step_dt", c.cfg.decimation * c.cfg.dt),
+                  ("literal_layout", c.cfg.literal_layout), ("pdipm_iterations", c.cfg.pdipm_iterations),
+                  ("y0", c.cfg.y0), ("keep_solution", c.cfg.keep_solution))
+        return tuple((n, t.data_ptr()) for n, t in src) + consts
 
     def __call__(self) -> Tuple[torch.Tensor, torch.Tensor]:
         if self.c._version != self._version:
             raise RuntimeError("GraphedMPCStep: a controller setter replaced a captured tensor since the "
                                "capture; update tensors in place, or capture a new GraphedMPCStep")
+        sig = self._current_signature()
+        if sig != self._signature:
+            changed = [a[0] for a, b in zip(sig, self._signature) if a != b]
+            raise RuntimeError(f"GraphedMPCStep: {', '.join(changed)} replaced or changed since the capture "
+                               "(the graph would read the captured values); update tensors in place, or "
+                               "capture a new GraphedMPCStep")
         self.graph.replay()
         return self.c.foot_wrench, self.c.cost
 

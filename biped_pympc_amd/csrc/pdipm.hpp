@@ -43,6 +43,10 @@ struct SolverArgs {
   double y0;
 };
 
+// iterative-refinement steps per direction in the LDS-resident and general kernels (the register
+// kernels' one step sits at the FP64 floor at N = 10 / 20)
+constexpr int kRefineSteps = 2;
+
 constexpr unsigned long long kFallbackBits = 0x7FF8DEADBEEF5A5Aull;  // quiet NaN with a payload
 
 __device__ inline const double* solver_in(const SolverArgs& a, int i) {
@@ -341,11 +345,26 @@ struct SolverCtx {
     }
   }
 
-  // One step of iterative refinement of the combined direction (derivation at pdipm_srbd_reg.hpp
-  // RegCtx::refine_rhs): RX <- RX + (H + beta) dx + G^T dz + A^T dy, RE <- RE + A dx - delta dy
-  // (minus the residual of KKT rows 1 and 4; rows 2 and 3 hold by construction), dx and dy saved
-  // to the output rows for solve(true).
+  // One step of iterative refinement of a direction against the full KKT from the residuals of all
+  // four rows (pdipm_srbd.hpp FastCtx::refine_rhs has the scheme, pdipm_srbd_reg.hpp RegCtx::refine_rhs
+  // the derivation): step 0 per inequality row q = D^-1 (e2 - W e3), VV += q, RS -= e3, DZ += q; then
+  // RX <- -(e1 - G^T q) (G^T over the updated DZ), RE <- -e4; dx and dy saved to the output rows for
+  // solve(true). RX, RE, RS are overwritten (the caller restores them with residuals() after
+  // refining the affine direction).
   __device__ void refine_rhs() {
+    for (int q = lane; q < m; q += 64) {  // step 0 (rows 2 and 3)
+      const int i = q / 16, k = q % 16;
+      double gd = 0.0;
+      for (int t = 0; t < c_tab.gr_n[k]; ++t)
+        gd += G(i, c_tab.gr_off[k][t]) * TV[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
+      const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
+      const double qc = DI[q] * (e2 - WD[q] * e3);
+      VV[q] = VV[q] + qc;
+      RS[q] = RS[q] - e3;
+      DZ[q] = DZ[q] + qc;
+    }
+    __syncthreads();
     for (int e = lane; e < nz; e += 64) xsg[e] = TV[e];
     for (int e = lane; e < p; e += 64) ysg[e] = DY[e];
     for (int c = lane; c < nz; c += 64) {
@@ -401,8 +420,9 @@ struct SolverCtx {
   // ------------------------------------------------------------------------- solve ----
   // Solves K [dx; ds; dz; dy] = [-RX; R2; -RS; -RE] with the current factors.
   // Result: dx -> TV, ds -> DS, dz -> DZ, dy -> DY.
-  // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV kept from the
-  // combined solve), then dx = saved + correction before dz, ds are formed; DY is the correction.
+  // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV, RS from refine_rhs's
+  // step 0 carry rows 2 and 3), then dx = saved + correction before dz, ds are formed; DY is the
+  // correction.
   __device__ void solve(bool ref = false) {
     if (!ref)
       for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
@@ -571,6 +591,19 @@ struct SolverCtx {
     __syncthreads();
   }
 
+  // kRefineSteps refinement steps (pdipm_srbd.hpp FastCtx::refine: later steps restore the original
+  // right-hand side and refine from the full dy = saved + correction)
+  __device__ void refine() {
+    for (int step = 0; step < kRefineSteps; ++step) {
+      if (step > 0) {
+        for (int e = lane; e < p; e += 64) DY[e] = ysg[e] + DY[e];
+        residuals();
+      }
+      refine_rhs();
+      solve(true);
+    }
+  }
+
   // fmax(fmin(1, 0.99 * min_i if_else(dv_i < 0, -v_i/dv_i, 1)), 1e-12)  (:460-467)
   __device__ double step_length(const double* v, const double* dv) const {
     double mn = INFINITY;
@@ -651,11 +684,20 @@ __device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
+    // a degenerate iterate (some s at its 1e-8 clamp) also refines the affine direction
+    // (pdipm_srbd.hpp, pdipm_srbd_reg.hpp main loops); one wave per QP: a wave-uniform vote
+    bool sclamp = false;
+    for (int q = lane; q < m; q += 64) sclamp = sclamp || (C.S[q] <= 1e-8);
+    const bool degen = __any(sclamp);
     C.factor();
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
     C.solve();
+    if (degen) {
+      C.refine();
+      C.residuals();  // restores RX, RS, RE for the combined solve
+    }
     const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
     double sza = 0.0;
     for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
@@ -669,8 +711,7 @@ __device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
     }
     __syncthreads();
     C.solve();
-    C.refine_rhs();
-    C.solve(true);
+    C.refine();
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
     __syncthreads();
     double szn = 0.0;

@@ -23,7 +23,7 @@ namespace srbd {
 
 
 struct FastLayout {
-  int Md, Nd, Cd, Gd, K0, K1, Pd, IX, Hu, SG, PH, DV, X, S, Z, Y, RX, RS, RE, WD, DI, VV, TV, QV, WV,
+  int Md, Nd, Cd, Gd, K0, K1, Pd, IX, Hu, SG, PH, DV, X, S, Z, Y, RX, RS, RE, WD, DI, VV, R2, TV, QV, WV,
       DS, DZ, DY, SC, total;
   __host__ __device__ FastLayout(int N) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
@@ -34,7 +34,7 @@ struct FastLayout {
     PH = take(20 * N); DV = take(78 * N);
     X = take(nz); S = take(m); Z = take(m); Y = take(p);
     RX = take(nz); RS = take(m); RE = take(p);
-    WD = take(m); DI = take(m); VV = take(m);
+    WD = take(m); DI = take(m); VV = take(m); R2 = take(m);
     TV = take(nz); QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
     SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector
@@ -67,13 +67,15 @@ __device__ __forceinline__ int perm12(int j) { return j < 6 ? j + 6 : j - 6; }
 // acc += v[lane K of this 16-lane row] * c in one instruction (measured 8-9 issue cycles vs ~11 for
 // v_mov_b64_dpp + v_fmac_f64; scripts/microbench_fp64.hip). LLVM does not form these itself, so
 // they are inline asm; an asm block is invisible to the hazard recognizer, hence the s_nop 1 on
-// entry (VALU write -> DPP read needs 2 wait states). Inside a block no instruction reads a
-// register an earlier one in the block wrote.
-// No wait states at the END of a block: a DPP the compiler emits after a block gets its own from
-// the hazard recognizer (it treats the block's outputs as VALU writes), and every block starts with
-// its own s_nop 1 for the DPP inside it. Dropping the trailing s_nop 1 of every block (231 per N=10
-// step kernel) was bit-identical and 1.5 % (N = 10) / 2.0 % (N = 20) faster;
-// -DSRBD_ASM_TAIL='"s_nop 1\n"' restores it (A/B switch).
+// entry (VALU write -> DPP read needs 2 wait states, for EVERY VGPR the DPP reads, its fmac
+// accumulator included). Inside a block a DPP reads no register written by one of the 2
+// instructions before it (independent accumulators, or an s_nop 0 between).
+// No wait states at the END of a block: the safeguard for a DPP the compiler emits after a block is
+// the static audit of the final ISA (tests/test_isa_hazards.py, scripts/dpp_hazard_check.py: every
+// DPP operand, every control-flow predecessor), not the hazard recognizer, which does not model
+// inline asm. Dropping the trailing s_nop 1 of every block (231 per N=10 step kernel) was
+// bit-identical and 1.5 % (N = 10) / 2.0 % (N = 20) faster; -DSRBD_ASM_TAIL='"s_nop 1\n"' restores
+// it (A/B switch).
 #ifndef SRBD_ASM_TAIL
 #define SRBD_ASM_TAIL ""
 #endif
@@ -181,7 +183,7 @@ template <int NT>  // NT > 0: horizon fixed at compile time (all trip counts con
 struct FastCtx {
   int N_, lane;
   double *Md, *Nd, *Cd, *Gd, *K0, *K1, *Pd, *IX, *Hu, *SG, *PH, *DV, *X, *S, *Z, *Y, *RX, *RS, *RE, *WD,
-      *DI, *VV, *TV, *QV, *WV, *DS, *DZ, *DY, *SC;
+      *DI, *VV, *R2, *TV, *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
   double *xsg, *ysg;  // this QP's x / y output rows: the saved dx / dy during the refinement solve
   PROF_DECL
@@ -419,12 +421,31 @@ struct FastCtx {
     PROF_ADD(2);
   }
 
-  // One step of iterative refinement of the combined direction (pdipm_srbd_reg.hpp RegCtx::refine_rhs
-  // has the derivation): r_x <- r_x + (H + beta) dx + G^T dz + A^T dy, r_e <- r_e + A dx - delta dy,
-  // i.e. minus the residual of KKT rows 1 and 4; dx, dy saved to the output rows for solve(2).
+  // One step of iterative refinement of a direction d = (dx, ds, dz, dy) against the full KKT of
+  // sparse_pdipm_solver.py:412-439, from the residuals of all four KKT rows (derivation at
+  // pdipm_srbd_reg.hpp RegCtx::refine_rhs; rows 1 + 4 alone stall at ~1e-6 at degenerate iterates,
+  // profiles/r02/refinement_4row.txt):
+  //   e1 = -r_x - (H + beta) dx - G^T dz - A^T dy,   e2 = r2 - (W ds + dz),
+  //   e3 = -r_s - (G dx + ds - delta dz),           e4 = -r_e - (A dx - delta dy).
+  // Step 0, per inequality row: q = D^-1 (e2 - W e3); VV += q and r_s -= e3, so solve(2)'s
+  // re-formation dz = VV + Lambda G dx, ds = -r_s - G dx + delta dz yields dz + c_z, ds + c_s; dz += q
+  // so that G^T (dz + q) folds the reduced right-hand side e1 - G^T q into row 1. Then
+  // RX <- -(e1 - G^T q), RE <- -e4, dx and dy saved to the output rows for solve(2).
+  // RX, RE and RS are overwritten: the caller restores them (residuals()) when the direction refined
+  // is the affine one and the combined solve still needs them.
   __device__ void refine_rhs() {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
-    (void)m;
+    for (int q = lane; q < m; q += 64) {  // step 0 (rows 2 and 3)
+      const int i = q / 16, k = q % 16;
+      const double gd = dotrow12(Gd + 12 * k, TV + 12 * N + 12 * i);
+      const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
+      const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
+      const double qc = DI[q] * (e2 - WD[q] * e3);
+      VV[q] = VV[q] + qc;
+      RS[q] = RS[q] - e3;
+      DZ[q] = DZ[q] + qc;
+    }
+    __syncthreads();
     for (int e = lane; e < nz; e += 64) xsg[e] = TV[e];
     for (int e = lane; e < p; e += 64) ysg[e] = DY[e];
     for (int c = lane; c < nz; c += 64) {
@@ -466,7 +487,7 @@ struct FastCtx {
 
   // ------------------------------------------------------------------------ solve ----
   // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu);
-  // mode 2: the refinement solve (rhs from refine_rhs, VV kept from mode 1, dx = saved + correction)
+  // mode 2: the refinement solve (rhs from refine_rhs, VV from refine_rhs's step 0, dx = saved + correction)
   __device__ void solve(int mode, double smu) {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
     (void)nz; (void)m; (void)p;
@@ -476,6 +497,7 @@ struct FastCtx {
         const double si = 1.0 / S[q];
         double r2 = -(si * (S[q] * Z[q]));
         if (mode) r2 = r2 + -(si * (S[q] * Z[q] + DS[q] * DZ[q] - smu));
+        R2[q] = r2;  // row 2's right-hand side for refine_rhs
         VV[q] = DI[q] * (r2 + WD[q] * RS[q]);
       }
     }
@@ -673,6 +695,24 @@ struct FastCtx {
     PROF_ADD(3);
   }
 
+  // kRefineSteps steps of iterative refinement of the direction just solved (affine or combined).
+  // Each step after the first restores the original right-hand side (residuals(): r_x, r_s, r_e;
+  // r2 stays in R2) and takes the full dy = saved + correction, so the next refine_rhs measures the
+  // residual of the ORIGINAL system at the refined direction. One step leaves the longer horizons
+  // (N = 32: 20x the FP64 floor at K = 1) and N = 1 on the general kernel above the floor; two reach
+  // it (tests/test_gpu_parity.py::test_runtime_horizon_solver_matches_oracle).
+  __device__ void refine() {
+    const int N = NT > 0 ? NT : N_, p = 14 * N;
+    for (int step = 0; step < kRefineSteps; ++step) {
+      if (step > 0) {
+        for (int e = lane; e < p; e += 64) DY[e] = ysg[e] + DY[e];
+        residuals();
+      }
+      refine_rhs();
+      solve(2, 0.0);
+    }
+  }
+
   __device__ double step_length(const double* v, const double* dv) const {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
     (void)nz; (void)m; (void)p;
@@ -702,7 +742,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   C.Hu = smem + Lo.Hu; C.SG = smem + Lo.SG; C.PH = smem + Lo.PH; C.DV = smem + Lo.DV;
   C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
   C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE; C.WD = smem + Lo.WD; C.DI = smem + Lo.DI;
-  C.VV = smem + Lo.VV; C.TV = smem + Lo.TV; C.QV = smem + Lo.QV; C.WV = smem + Lo.WV;
+  C.VV = smem + Lo.VV; C.R2 = smem + Lo.R2; C.TV = smem + Lo.TV; C.QV = smem + Lo.QV; C.WV = smem + Lo.WV;
   C.DS = smem + Lo.DS; C.DZ = smem + Lo.DZ; C.DY = smem + Lo.DY; C.SC = smem + Lo.SC;
   const int nz = 24 * N, m = 16 * N, p = 14 * N, nA = nnz_A(N), nG = 28 * N;
   const double* Hg = solver_in(args, 0) + (size_t)env * nz;
@@ -814,9 +854,19 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
+    // a degenerate iterate (some s at its 1e-8 clamp, sparse_pdipm_solver.py:520) also refines the
+    // affine direction: its ds, dz lose most digits where W = z / s ~ 1e8 and enter sigma and the
+    // corrector (pdipm_srbd_reg.hpp main loop; one wave per QP: a wave-uniform vote)
+    bool sclamp = false;
+    for (int q = lane; q < m; q += 64) sclamp = sclamp || (C.S[q] <= 1e-8);
+    const bool degen = __any(sclamp);
     PROF_ADD_CTX(C, 0);
     C.factor();
     C.solve(0, 0.0);
+    if (degen) {
+      C.refine();
+      C.residuals();  // restores r_x, r_s, r_e for the combined solve
+    }
     const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
     double sza = 0.0;
     for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
@@ -825,8 +875,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
     __syncthreads();
     PROF_ADD_CTX(C, 5);
     C.solve(1, sigma * mu * 1.0);
-    C.refine_rhs();
-    C.solve(2, 0.0);
+    C.refine();
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
     __syncthreads();
     double szn = 0.0;

@@ -211,12 +211,15 @@ struct CoupleRow {
   double d, b, a0, a1, a2;
 };
 // Both with two accumulators (short dependent paths); the forward form folds the subtraction from
-// the right-hand side into its first FMA: base - C w, and C^T y.
+// the right-hand side into its first FMA: base - C w, and C^T y. A DPP instruction must not read ANY
+// VGPR -- its fmac accumulator included -- written in the 2 wait states before it (the rule LLVM's
+// hazard recognizer applies to every DPP operand; scripts/dpp_hazard_check.py audits the final ISA),
+// hence the s_nop 0 before an accumulator's second FMA.
 __device__ __forceinline__ double couple_cw_sub(const CoupleRow& c, double w, double base) {
   double a1 = fma(-c.d, w, base);
   double a2 = -c.b * shl6(w);
   asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "-%3", 6) SRBD_FMAC_BC("%1", "%2", "-%4", 7)
-      SRBD_FMAC_BC("%0", "%2", "-%5", 8) SRBD_ASM_TAIL
+      "s_nop 0\n" SRBD_FMAC_BC("%0", "%2", "-%5", 8) SRBD_ASM_TAIL
       : "+v"(a1), "+v"(a2)
       : "v"(w), "v"(c.a0), "v"(c.a1), "v"(c.a2));
   return a1 + a2;
@@ -225,20 +228,24 @@ __device__ __forceinline__ double couple_cty2(const CoupleRow& c, double y) {
   double a1 = c.d * y;
   double a2 = c.b * shr6(y);
   asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%2", "%3", 0) SRBD_FMAC_BC("%1", "%2", "%4", 1)
-      SRBD_FMAC_BC("%0", "%2", "%5", 2) SRBD_ASM_TAIL
+      "s_nop 0\n" SRBD_FMAC_BC("%0", "%2", "%5", 2) SRBD_ASM_TAIL
       : "+v"(a1), "+v"(a2)
       : "v"(y), "v"(c.a0), "v"(c.a1), "v"(c.a2));
   return a1 + a2;
 }
 // init - sum_j c[j] v(lane j) over the 12 rows of a 16-lane DPP row: two accumulators (the
-// broadcast-FMAs issue every 8 cycles, so each accumulator's FMAs are 16 cycles apart) and one add
+// broadcast-FMAs issue every 8 cycles, so each accumulator's FMAs are 16 cycles apart) and one add;
+// an s_nop 0 after each pair keeps 2 wait states between an accumulator's write and its next DPP
+// read (a third accumulator would cost 2 VGPRs the N = 20 kernels do not have)
 __device__ __forceinline__ double dot_bc12_sub(const double (&c)[12], double v, double init) {
   double a0 = init, a1 = 0.0;
   asm("s_nop 1\n"
-      SRBD_FMAC_BC("%0", "%2", "-%3", 0) SRBD_FMAC_BC("%1", "%2", "-%4", 1) SRBD_FMAC_BC("%0", "%2", "-%5", 2)
-      SRBD_FMAC_BC("%1", "%2", "-%6", 3) SRBD_FMAC_BC("%0", "%2", "-%7", 4) SRBD_FMAC_BC("%1", "%2", "-%8", 5)
-      SRBD_FMAC_BC("%0", "%2", "-%9", 6) SRBD_FMAC_BC("%1", "%2", "-%10", 7) SRBD_FMAC_BC("%0", "%2", "-%11", 8)
-      SRBD_FMAC_BC("%1", "%2", "-%12", 9) SRBD_FMAC_BC("%0", "%2", "-%13", 10) SRBD_FMAC_BC("%1", "%2", "-%14", 11)
+      SRBD_FMAC_BC("%0", "%2", "-%3", 0) SRBD_FMAC_BC("%1", "%2", "-%4", 1) "s_nop 0\n"
+      SRBD_FMAC_BC("%0", "%2", "-%5", 2) SRBD_FMAC_BC("%1", "%2", "-%6", 3) "s_nop 0\n"
+      SRBD_FMAC_BC("%0", "%2", "-%7", 4) SRBD_FMAC_BC("%1", "%2", "-%8", 5) "s_nop 0\n"
+      SRBD_FMAC_BC("%0", "%2", "-%9", 6) SRBD_FMAC_BC("%1", "%2", "-%10", 7) "s_nop 0\n"
+      SRBD_FMAC_BC("%0", "%2", "-%11", 8) SRBD_FMAC_BC("%1", "%2", "-%12", 9) "s_nop 0\n"
+      SRBD_FMAC_BC("%0", "%2", "-%13", 10) SRBD_FMAC_BC("%1", "%2", "-%14", 11)
       SRBD_ASM_TAIL
       : "+v"(a0), "+v"(a1)
       : "v"(v), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),

@@ -191,6 +191,8 @@ int srbd_set_solver_path(int path) {
   return 0;
 }
 
+int srbd_get_solver_path(void) { return solver_path(); }
+
 size_t srbd_mpc_workspace_doubles(int horizon, int batch) {
   if (!horizon_ok(horizon) || batch < 0) return 0;
   const size_t N = (size_t)horizon;

@@ -143,9 +143,12 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     if buffers.workspace.device != former_inputs[0].device:
         raise ValueError(f"mpc_solve: workspace on {buffers.workspace.device}, inputs on {former_inputs[0].device}")
     L = _native.lib()
+    # the fused kernel runs only at N = 10 / 20 under the auto solver path; otherwise the former
+    # writes the whole QP into the workspace for the solver kernel
+    one_kernel = fused and N in (10, 20) and _native.current_solver_path() == 0
     rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
                           _native.ptr_array([t.data_ptr() for t in former_inputs]),
-                          buffers.workspace.data_ptr() if (keep_qp or not fused or N not in (10, 20)) else None,
+                          buffers.workspace.data_ptr() if (keep_qp or not one_kernel) else None,
                           _native.ptr_array([t.data_ptr() for t in buffers.outputs]), _stream_ptr())
     _native.check(rc, "srbd_mpc_solve")
     return buffers.outputs

@@ -103,6 +103,10 @@ size_t srbd_solver_lds_bytes(int horizon);
  * library keeps between calls -- configured kernel LDS limits, the blocking calls' events, the
  * solver path -- is kept per device (csrc/device_state.hpp). */
 int srbd_set_solver_path(int path);
+/* The solver path in effect for the current HIP device (0 if never set). srbd_mpc_solve_fused under a
+ * non-auto path runs srbd_mpc_solve and so needs qp_workspace; srbd_mpc_step always runs the fused
+ * register kernel (its QPs are stage-invariant by construction) and ignores the path. */
+int srbd_get_solver_path(void);
 
 /* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
  * offset maps the kernels use to address A_val/G_val. colptr has 24*horizon+1 entries, rowind nnz.

@@ -1,8 +1,11 @@
 """Static check of the VALU-write -> DPP-read hazard (2 wait states) in a kernel's ISA, inline asm
 included: for every DPP instruction, the instructions issued in the 2 wait states before it must not
-write a VGPR it reads. s_nop N counts N + 1 states, other instructions 1; the scan follows the
-straight-line predecessor and stops at a label (a branch target's other predecessors are not
-followed). Used to audit the asm blocks' wait states (csrc/pdipm_srbd.hpp SRBD_ASM_TAIL).
+write ANY VGPR it reads -- the DPP-routed src0, the other sources and, for v_fmac/v_mac, the
+accumulator (src2 = vdst). That is LLVM's GCNHazardRecognizer rule (every VGPR use of a DPP
+instruction), which the asm blocks cannot rely on the compiler to enforce. s_nop N counts N + 1
+states, other instructions 1. The scan walks back along every control-flow predecessor: the
+fall-through instruction (unless it is an unconditional s_branch / s_endpgm / s_setpc) and every
+branch that targets a label it crosses.
 
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -DSRBD_SPLIT_REG20 --cuda-device-only -S \
         -o /tmp/k.s biped_pympc_amd/csrc/srbd_mpc.hip
@@ -12,6 +15,8 @@ import re
 import sys
 
 REG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+BRANCH = re.compile(r"^s_(c?branch\w*|cbranch\w*)\s+(\S+)")
+NOFALL = ("s_branch", "s_endpgm", "s_setpc_b64")
 
 
 def regs(text):
@@ -25,19 +30,19 @@ def regs(text):
 
 
 def parse(lines):
-    """(kind, dst_regs, src_regs, text, states) per line; kind: 'label', 'inst', 'skip'."""
+    """(kind, dst_regs, src_regs, text, states, op, label) per line; kind: 'label', 'inst', 'skip'."""
     out = []
     for raw in lines:
         s = raw.split(";")[0].strip()
-        if not s or s.startswith(".") or s.startswith("//"):
-            out.append(("skip", set(), set(), raw, 0))
+        if s.endswith(":") and " " not in s:  # labels (.LBB0_2: included) before directives
+            out.append(("label", set(), set(), raw, 0, "", s[:-1]))
             continue
-        if s.endswith(":"):
-            out.append(("label", set(), set(), raw, 0))
+        if not s or s.startswith(".") or s.startswith("//"):
+            out.append(("skip", set(), set(), raw, 0, "", None))
             continue
         op, _, rest = s.partition(" ")
         if op == "s_nop":
-            out.append(("inst", set(), set(), raw, int(rest.strip(), 0) + 1))
+            out.append(("inst", set(), set(), raw, int(rest.strip(), 0) + 1, op, None))
             continue
         ops = [o.strip() for o in rest.split(",")] if rest else []
         dst, src = set(), set()
@@ -51,11 +56,41 @@ def parse(lines):
                     src |= dst
         else:
             src = regs(rest)
-        out.append(("inst", dst, src, raw, 1))
+        m = BRANCH.match(s)
+        out.append(("inst", dst, src, raw, 1, op, m.group(2) if m else None))
     return out
 
 
-def check(path, want=""):
+def dpp_reads(raw):
+    """Every VGPR a DPP instruction reads (sources, and the accumulator of v_fmac/v_mac)."""
+    s = raw.split(";")[0].strip()
+    op, _, rest = s.partition(" ")
+    ops = [o.strip() for o in rest.split(",")]
+    reads = set()
+    for o in ops[1:]:
+        reads |= regs(o.split(" ")[0])
+    if ("fmac" in op or "mac_" in op) and ops:
+        reads |= regs(ops[0])
+    return reads
+
+
+def _preds(ins, branches_to):
+    """Control-flow predecessors of instruction index i, as a function."""
+    def preds(i):
+        out = []
+        j = i - 1
+        # labels between i and its fall-through predecessor: every branch to them is a predecessor
+        while j >= 0 and ins[j][0] != "inst":
+            if ins[j][0] == "label":
+                out.extend(branches_to.get(ins[j][6], ()))
+            j -= 1
+        if j >= 0 and ins[j][5] not in NOFALL:
+            out.append(j)
+        return out
+    return preds
+
+
+def check(path, want="", verbose=True):
     lines = open(path).read().split("\n")
     bad = 0
     n_dpp = 0
@@ -76,32 +111,34 @@ def check(path, want=""):
         if want not in name:
             continue
         ins = parse(body)
-        for i, (kind, dst, src, raw, _) in enumerate(ins):
-            if kind != "inst" or "_dpp" not in raw.split(";")[0]:
+        branches_to = {}
+        for j, t in enumerate(ins):
+            if t[0] == "inst" and t[6] is not None:
+                branches_to.setdefault(t[6], []).append(j)
+        preds = _preds(ins, branches_to)
+        for i, t in enumerate(ins):
+            if t[0] != "inst" or "_dpp" not in t[3].split(";")[0]:
                 continue
             n_dpp += 1
-            s = raw.split(";")[0].strip()
-            op, _, rest = s.partition(" ")
-            ops = [o.strip() for o in rest.split(",")]
-            # the DPP-routed operand, src0 (the second operand of v_*_dpp D, S0, ...). The blocks'
-            # accumulator chains read their FMAC accumulator (src2 = D) 1-2 states after writing it,
-            # as they have since round 1 with results at the oracle's FP64 floor: the hardware
-            # hazard is on the routed operand (LLVM's recognizer checks every VGPR use)
-            reads = regs(ops[1]) if len(ops) > 1 else set()
-            states = 0
-            j = i - 1
-            while j >= 0 and states < 2:
-                k2, d2, _, r2, st = ins[j]
-                if k2 == "label":
+            reads = dpp_reads(t[3])
+            # depth-first over predecessors while fewer than 2 wait states separate them from i
+            stack = [(p, 0) for p in preds(i)]
+            seen = set()
+            while stack:
+                j, states = stack.pop()
+                if (j, states) in seen:
+                    continue
+                seen.add((j, states))
+                _, d2, _, r2, st, _, _ = ins[j]
+                if d2 & reads:
+                    bad += 1
+                    if verbose:
+                        print(f"{name}: {r2.strip()}  ->  {t[3].strip()}  ({states} states)")
                     break
-                if k2 == "inst":
-                    if d2 & reads:
-                        bad += 1
-                        print(f"{name}: {r2.strip()}  ->  {raw.strip()}  ({states} states)")
-                        break
-                    states += st
-                j -= 1
-    print(f"checked {n_dpp} DPP instructions, {bad} hazards")
+                if states + st < 2:
+                    stack.extend((p, states + st) for p in preds(j))
+    if verbose:
+        print(f"checked {n_dpp} DPP instructions, {bad} hazards")
     return bad
 
 

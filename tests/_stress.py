@@ -26,10 +26,18 @@ STRESS_CASES = {
     "tilt_N10": (10, dict(tilt=0.6, random_gait=True, residuals=True)),
     # residual accelerations of std 3 m/s^2 / 3 rad/s^2 (6x the SURVEY spread), randomized gait
     "push_N20": (20, dict(random_gait=True, residuals=True, residual_scale=3.0)),
+    # horizons without a register kernel (the runtime-N LDS-resident kernel under the auto path):
+    # flight at N = 5, and the right foot in swing over a 32-stage horizon with tilt and residuals
+    "flight_N5": (5, dict(contact_override=_contact(STRESS_B, 5, 0, 0))),
+    "swing_right_N32": (32, dict(contact_override=_contact(STRESS_B, 32, 1, 0), tilt=0.3, residuals=True)),
 }
+
+
+# fixed seeds (the first four are the round-2 cases' seeds, 9000 + their sorted position then)
+_SEEDS = {"flight_N10": 9000, "push_N20": 9001, "swing_left_N20": 9002, "tilt_N10": 9003,
+          "flight_N5": 9004, "swing_right_N32": 9005}
 
 
 def stress_workload(name):
     N, kw = STRESS_CASES[name]
-    seed = 9000 + sorted(STRESS_CASES).index(name)
-    return N, make_workload(STRESS_B, N, seed=seed, **kw)
+    return N, make_workload(STRESS_B, N, seed=_SEEDS[name], **kw)

@@ -320,6 +320,7 @@ def test_one_launch_step_equals_three_kernels(N, gait, literal, torque):
     c1 = _controller(B, N, st, cmd, ctrl, params, gait_args, table, literal)
     c2 = _controller(B, N, st, cmd, ctrl, params, gait_args, table, literal)
     c1.cfg.keep_solution = True
+    c2.cfg.keep_solution = True
     J, cb = (torch.from_numpy(a) for a in _torque_inputs(B, ndof, 9))
     for step in range(3):
         if torque:
@@ -371,3 +372,22 @@ def test_graphed_step_refuses_stale_or_converted_tensors():
     c.set_contact_table(torch.from_numpy(table))  # replaces a captured tensor
     with pytest.raises(RuntimeError, match="replaced"):
         g()
+    # direct field assignment, as the reference's StateEstimator.set_body_state and
+    # mpc_wrapper.set_srbd_accel do, bypasses the setters: the replay still refuses
+    g = GraphedMPCStep(c)
+    g()
+    c.state_estimate_data.root_position = c.state_estimate_data.root_position.clone()
+    with pytest.raises(RuntimeError, match="root_position"):
+        g()
+    g = GraphedMPCStep(c)
+    c.residual_lin_accel = c.residual_lin_accel.clone()
+    with pytest.raises(RuntimeError, match="residual_lin_accel"):
+        g()
+    g = GraphedMPCStep(c)
+    c.mass = c.mass * 1.1  # a constant the graph baked in
+    with pytest.raises(RuntimeError, match="mass"):
+        g()
+    c.mass = c.mass / 1.1
+    g = GraphedMPCStep(c)
+    c.state_estimate_data.root_position.add_(0.01)  # in-place updates stay fine
+    g()

@@ -1,10 +1,13 @@
 """Static audit of the DPP wait states in the product kernels (CPU only: hipcc cross-compiles).
 
 The broadcast-FMA asm blocks (csrc/pdipm_srbd.hpp SRBD_FMAC_BC) open with `s_nop 1` and carry no
-trailing wait states; the compiler pads its own DPPs after a block. A wrong wait state gives wrong
-values with no fault, and possibly only under some wave interleavings, so the final ISA of both
-translation units is checked: no DPP instruction reads a VGPR written within the 2 wait states before
-it (scripts/dpp_hazard_check.py; a planted hazard is detected by the same checker).
+trailing wait states, and inside a block a DPP reads no VGPR written by either of the 2 instructions
+before it. A wrong wait state gives wrong values with no fault, and possibly only under some wave
+interleavings, so the final ISA of both translation units -- compiled with the product build's own
+flags (biped_pympc_amd/build.py unit_compile_cmd) -- is checked: no DPP instruction reads ANY VGPR
+(routed source, other sources, fmac accumulator) written within the 2 wait states before it, along
+every control-flow predecessor (scripts/dpp_hazard_check.py; planted hazards are detected by the same
+checker). Where hipcc exists the audit must run: it fails rather than skips.
 """
 import os
 import shutil
@@ -15,32 +18,43 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-CSRC = os.path.join(ROOT, "biped_pympc_amd", "csrc")
 
 
-def _isa(tmp_path, unit, flags):
+def _isa(tmp_path, unit):
+    from biped_pympc_amd.build import HIPCC, unit_compile_cmd
+    if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
+        pytest.skip("hipcc not available")
     out = tmp_path / (unit + ".s")
-    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
-           "--cuda-device-only", "-S", "-o", str(out), os.path.join(CSRC, unit)] + flags
+    cmd = unit_compile_cmd(unit, ["--cuda-device-only", "-S", "-o", str(out)])
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     return str(out)
 
 
-@pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="hipcc not available")
-@pytest.mark.parametrize("unit,flags", [
-    ("srbd_mpc.hip", ["-DSRBD_SPLIT_REG20"]),  # the main unit as biped_pympc_amd/build.py builds it
-    ("srbd_reg20.hip", ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]),
-])
-def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit, flags):
+@pytest.mark.parametrize("unit", ["srbd_mpc.hip", "srbd_reg20.hip"])
+def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
     from dpp_hazard_check import check
-    assert check(_isa(tmp_path, unit, flags)) == 0
+    assert check(_isa(tmp_path, unit)) == 0
 
 
-def test_checker_detects_a_planted_hazard(tmp_path):
+def test_checker_detects_planted_hazards(tmp_path):
     from dpp_hazard_check import check
-    p = tmp_path / "t.s"
-    p.write_text("_Zk:\n\tv_add_f64 v[2:3], v[4:5], v[6:7]\n\ts_nop 0\n"
-                 "\tv_mov_b64_dpp v[8:9], v[2:3] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\ts_endpgm\n")
-    assert check(str(p)) == 1
+    cases = {
+        # routed source written 1 state before
+        "src0": "_Zk:\n\tv_add_f64 v[2:3], v[4:5], v[6:7]\n\ts_nop 0\n"
+                "\tv_mov_b64_dpp v[8:9], v[2:3] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\ts_endpgm\n",
+        # fmac accumulator written by the previous instruction
+        "acc": "_Zk:\n\tv_fmac_f64_dpp v[2:3], v[4:5], v[6:7] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+               "\tv_fmac_f64_dpp v[2:3], v[4:5], v[8:9] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\ts_endpgm\n",
+        # written before a branch whose target is right in front of the DPP
+        "branch": "_Zk:\n\tv_add_f64 v[2:3], v[4:5], v[6:7]\n\ts_branch .LBB0_2\n\ts_nop 7\n.LBB0_2:\n"
+                  "\tv_mov_b64_dpp v[8:9], v[2:3] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\ts_endpgm\n",
+    }
+    for name, text in cases.items():
+        p = tmp_path / f"{name}.s"
+        p.write_text(text)
+        assert check(str(p), verbose=False) == 1, name
+    ok = tmp_path / "ok.s"
+    ok.write_text("_Zk:\n\tv_add_f64 v[2:3], v[4:5], v[6:7]\n\ts_nop 1\n"
+                  "\tv_mov_b64_dpp v[8:9], v[2:3] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\ts_endpgm\n")
+    assert check(str(ok), verbose=False) == 0
