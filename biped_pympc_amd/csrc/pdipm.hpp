@@ -684,20 +684,13 @@ __device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
-    // a degenerate iterate (some s at its 1e-8 clamp) also refines the affine direction
-    // (pdipm_srbd.hpp, pdipm_srbd_reg.hpp main loops); one wave per QP: a wave-uniform vote
-    bool sclamp = false;
-    for (int q = lane; q < m; q += 64) sclamp = sclamp || (C.S[q] <= 1e-8);
-    const bool degen = __any(sclamp);
     C.factor();
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
     C.solve();
-    if (degen) {
-      C.refine();
-      C.residuals();  // restores RX, RS, RE for the combined solve
-    }
+    C.refine();  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
+    C.residuals();  // restores RX, RS, RE for the combined solve
     const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
     double sza = 0.0;
     for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);

@@ -854,19 +854,16 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
-    // a degenerate iterate (some s at its 1e-8 clamp, sparse_pdipm_solver.py:520) also refines the
-    // affine direction: its ds, dz lose most digits where W = z / s ~ 1e8 and enter sigma and the
-    // corrector (pdipm_srbd_reg.hpp main loop; one wave per QP: a wave-uniform vote)
-    bool sclamp = false;
-    for (int q = lane; q < m; q += 64) sclamp = sclamp || (C.S[q] <= 1e-8);
-    const bool degen = __any(sclamp);
+    // The affine direction is refined too: its ds, dz enter sigma and the corrector's right-hand
+    // side, which the combined direction's refinement cannot correct. The register kernels refine it
+    // only at degenerate iterates (an s at its clamp, W = z / s ~ 1e8); this kernel serves the
+    // longer horizons, where the unrefined affine direction already leaves K = 1 at 25x the FP64
+    // floor (N = 32, scripts/runtime_parity_probe.py), so it refines it in every iteration.
     PROF_ADD_CTX(C, 0);
     C.factor();
     C.solve(0, 0.0);
-    if (degen) {
-      C.refine();
-      C.residuals();  // restores r_x, r_s, r_e for the combined solve
-    }
+    C.refine();
+    C.residuals();  // restores r_x, r_s, r_e for the combined solve
     const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
     double sza = 0.0;
     for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
