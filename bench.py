@@ -41,6 +41,7 @@ WORK = {
 }
 PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD spec; no sparsity)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NODE_GPUS = int(os.environ.get("SRBD_NODE_GPUS", "8"))  # GPUs sharing one host (an 8-GPU MI355X node)
 
 
 def parse():
@@ -55,6 +56,9 @@ def parse():
     p.add_argument("--kernel-reps", type=int, default=10)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-full-host", action="store_true",
+                   help="also time the CPU baseline on every CPU the process may run on (off by default: "
+                        "the GPU box gives one GPU's job a 16-CPU share of the host)")
     p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
     return p.parse_args()
 
@@ -106,7 +110,7 @@ def load_sq(N: int, B: int, K: int):
             continue
         if (d.get("horizon") == N and d.get("batch") == B and d.get("iters") == K
                 and name in (d.get("kernel") or "") and d.get("utilisation")):
-            return dict(d["utilisation"], source=os.path.relpath(path, ROOT))
+            return dict(d["utilisation"], source=f"from {os.path.relpath(path, ROOT)} (rocprofv3 SQ counters, offline)")
     return None
 
 
@@ -119,6 +123,19 @@ def _cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def _physical_cores(cpus) -> int:
+    """Distinct (package, core) pairs among the logical CPUs `cpus` (SMT siblings count once)."""
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "physical_package_id") as f1, open(base + "core_id") as f2:
+                seen.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            seen.add(("?", str(c)))
+    return len(seen)
 
 
 def main():
@@ -234,14 +251,16 @@ def main():
         roofline = {
             "bound": "fp64-valu", "kernel": solver_kernel_name(N), "achieved": round(achieved, 4),
             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP64_TFLOPS, 6),
-            "traffic": traffic, "traffic_source": traffic_src,
+            # traffic and utilisation are NOT measured in this run: they are read from the committed
+            # rocprofv3 --pmc / SQ-counter summaries of the same kernel and configuration
+            "traffic": traffic, "traffic_source": traffic_src and f"from {traffic_src} (rocprofv3 --pmc, offline)",
             "algorithmic_flops_per_launch": flops, "launch_ms": round(ms_main, 4),
             "note": ("FP64 compute roof (vector == matrix peak on MI355X); the kernel runs on the "
                      "FP64 VALU (no MFMA): bound = its issue rate and the 12x12 chains. Flops = the reference's sparse-LDL KKT work per iteration "
                      "(SURVEY 8d) x iterations x QPs per launch. Bytes = former inputs in + "
                      "solution out per QP (fused step)." if fused else
                      "FP64 compute roof; flops as SURVEY 8d; bytes = QP in + solution out."),
-            "utilisation": load_sq(N, B, K),  # measured VALU / LDS busy shares (what bounds it)
+            "utilisation": load_sq(N, B, K),  # VALU / LDS busy shares from profiles/ (SQ counters, offline)
             "hbm": {"achieved_GBs": round(hbm_bytes / (ms_main * 1e-3) / 1e9, 2),
                     "peak_GBs": PEAK_HBM_GBS,
                     "frac": round(hbm_bytes / (ms_main * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
@@ -271,6 +290,20 @@ def main():
             t_cpu += dt
             solves += sample
         q1, med, q3 = np.percentile(sample / np.array(passes), [25, 50, 75])
+        aff_cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(host_cpus))
+        phys_host = _physical_cores(range(host_cpus))
+        phys_aff = _physical_cores(aff_cpus)
+        cores_used = min(threads, phys_aff)  # OpenMP threads spread over distinct physical cores first
+        full = None
+        if a.cpu_full_host:  # measured on every CPU of the affinity set (opt-in, see --help)
+            oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=affinity)
+            nf, tf = 0, 0.0
+            while tf < a.cpu_seconds / 2:
+                t1 = time.perf_counter()
+                oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=affinity)
+                tf += time.perf_counter() - t1
+                nf += sample
+            full = {"value": round(nf / tf, 1), "threads": affinity, "physical_cores": phys_aff}
         # BASELINE config 1 (B = 1, N = 10, K = 5: the reference's CPU-runnable case) on one core,
         # and B = 256 at the bench's K on the same CPU share
         one = [x[:1] for x in wl.inputs]
@@ -286,8 +319,16 @@ def main():
         t256 = time.perf_counter() - t1
         cpu = {"value": round(solves / t_cpu, 1), "unit": "solves/s", "cores": threads,
                "median": round(float(med), 1), "iqr": [round(float(q1), 1), round(float(q3), 1)],
-               "kind": "port", "per_core": round(solves / t_cpu / threads, 1),
-               "host": {"logical_cpus": host_cpus, "affinity_cpus": affinity, "model": _cpu_model()},
+               "kind": "port", "per_core": round(solves / t_cpu / cores_used, 1),
+               "per_core_basis": f"{cores_used} physical cores ({threads} OpenMP threads)",
+               "host": {"logical_cpus": host_cpus, "physical_cores": phys_host, "affinity_cpus": affinity,
+                        "affinity_physical_cores": phys_aff, "model": _cpu_model(),
+                        # one GPU's fair share of the host's physical cores, and the whole host, at the
+                        # measured per-core rate (linear scaling assumed: the envs are independent)
+                        "per_gpu_share_estimate": round(solves / t_cpu / cores_used * phys_host / NODE_GPUS, 1),
+                        "node_gpus": NODE_GPUS,
+                        "full_host_estimate": round(solves / t_cpu / cores_used * phys_host, 1),
+                        "full_host_measured": full},
                "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs, {threads} threads) on "
                           f"the first {sample} envs of the same workload, {solves // sample} passes, "
                           f"{t_cpu:.1f} s, N={N}, {K} iterations"),

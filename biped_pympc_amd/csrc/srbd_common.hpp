@@ -210,30 +210,11 @@ __host__ __device__ inline int a_pidx(const Tables& t, int N, int i, int r) {
   return (i < N - 1) ? a_xblock(i + 1) + t.cpx[r] : 36 * (N - 1) + r;
 }
 
-// ------------------------------------------------------- diagnostic phase stamps ----
-// Compiled in only with -DSRBD_PHASE_PROF (scripts/phase_profile.py builds a separate .so):
-// per-phase shader-clock cycles accumulated by lane 0 of every wave into g_phase_cycles.
-#ifdef SRBD_PHASE_PROF
-__device__ unsigned long long g_phase_cycles[16];
-#define PROF_DECL unsigned long long prof_t0_ = 0, prof_acc_[16] = {0};
-#define PROF_MARK() (prof_t0_ = __builtin_amdgcn_s_memtime())
-#define PROF_ADD(k)                                                  \
-  do {                                                               \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
-    prof_acc_[k] += t_ - prof_t0_;                                   \
-    prof_t0_ = t_;                                                   \
-  } while (0)
-#define PROF_FLUSH(ctx)                                              \
-  if (threadIdx.x == 0)                                              \
-    for (int k_ = 0; k_ < 16; ++k_) atomicAdd(&g_phase_cycles[k_], (ctx).prof_acc_[k_]);
-#define PROF_MARK_CTX(ctx) ((ctx).prof_t0_ = __builtin_amdgcn_s_memtime())
-#define PROF_ADD_CTX(ctx, k)                                         \
-  do {                                                               \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
-    (ctx).prof_acc_[k] += t_ - (ctx).prof_t0_;                       \
-    (ctx).prof_t0_ = t_;                                             \
-  } while (0)
-#else
+// ------------------------------------------------------------------ phase markers ----
+// Phase boundaries of the solver kernels, empty in the product build. The diagnostic builds of
+// scripts/phase_profile.py / isa_phase_mix.py / prologue_profile.py force-include
+// scripts/phase_prof.hpp (hipcc -include), which defines them first as s_memtime stamps.
+#ifndef PROF_DECL
 #define PROF_MARK_CTX(ctx)
 #define PROF_ADD_CTX(ctx, k)
 #define PROF_DECL

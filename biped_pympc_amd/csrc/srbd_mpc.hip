@@ -172,16 +172,6 @@ const char* srbd_last_error(void) { return g_last_error.c_str(); }
 
 size_t srbd_solver_lds_bytes(int horizon) { return horizon_ok(horizon) ? solver_lds_bytes(horizon) : 0; }
 
-#ifdef SRBD_PHASE_PROF
-// diagnostic build only: read and reset the per-phase cycle accumulators
-int srbd_debug_phase_cycles(unsigned long long* out16) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(srbd::g_phase_cycles), 16 * sizeof(unsigned long long)) != hipSuccess)
-    return -1;
-  unsigned long long z[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_phase_cycles), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 int srbd_set_solver_path(int path) {
   if (path < 0 || path > 2)
     return set_error(kErrInvalid, "srbd_set_solver_path: 0 (auto), 1 (general) or 2 (LDS-resident fast)");

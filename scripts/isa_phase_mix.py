@@ -2,12 +2,13 @@
 
 python scripts/isa_phase_mix.py [extra hipcc flags...]
 
-Builds the fused kernel with -DSRBD_PHASE_PROF (s_memtime stamps at the phase boundaries, see
+Builds the fused kernel with scripts/phase_prof.hpp force-included (s_memtime stamps at the phase boundaries, see
 srbd_common.hpp), splits the kernel's ISA at the stamps and counts instruction classes per
 segment: FP64 arithmetic, the inline-asm broadcast-FMAs, 32-bit integer/compare/select work
 (address and predicate arithmetic), moves, LDS and scalar instructions. Static counts of straight-
 line code equal per-iteration dynamic counts up to exec-skipped branches and the rolled loops.
 """
+import os
 import re
 import subprocess
 import sys
@@ -29,7 +30,7 @@ CLASSES = [
 def main():
     out = "/tmp/isa_phase_mix.s"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
-                    "--cuda-device-only", "-S", "-DSRBD_PHASE_PROF", *sys.argv[1:], "-o", out,
+                    "--cuda-device-only", "-S", "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), *sys.argv[1:], "-o", out,
                     f"{ROOT}/biped_pympc_amd/csrc/srbd_mpc.hip"], check=True, stderr=subprocess.DEVNULL)
     lines, on = [], False
     for ln in open(out):

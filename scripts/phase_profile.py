@@ -1,6 +1,6 @@
 """Diagnostic: per-phase cycle breakdown of the fast PDIPM kernel (s_memtime stamps).
 
-Builds a SEPARATE instrumented library (-DSRBD_PHASE_PROF) into /tmp and loads it via SRBD_LIB;
+Builds a SEPARATE instrumented library (scripts/phase_prof.hpp force-included) into /tmp and loads it via SRBD_LIB;
 the product library is untouched. Stamps serialise nothing but add a few instructions per phase.
 Run on the GPU box: python scripts/phase_profile.py [N] [B] [K]
 """
@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 LIB = "/tmp/libsrbd_mpc_prof.so"
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-DSRBD_PHASE_PROF", "-o", LIB, os.path.join(ROOT, "biped_pympc_amd/csrc/srbd_mpc.hip")],
+                "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), "-o", LIB, os.path.join(ROOT, "biped_pympc_amd/csrc/srbd_mpc.hip")],
                check=True)
 os.environ["SRBD_LIB"] = LIB
 

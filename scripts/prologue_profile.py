@@ -1,6 +1,6 @@
 """Diagnostic: shader-clock cycles of the fused kernel's prologue and epilogue per QP (GPU box).
 
-Builds a PATCHED COPY of csrc with -DSRBD_PHASE_PROF (the product sources are not touched) whose
+Builds a PATCHED COPY of csrc with scripts/phase_prof.hpp force-included (the product sources are not touched) whose
 extra stamps split the work before the Newton loop into: input read + former model, stage-block
 and f/b/d set-up, per-QP constants (C, K0, K1, slot tables), iterate init; and the work after it
 (outputs). The Newton iterations themselves are stamped as in scripts/phase_profile.py.
@@ -45,7 +45,7 @@ def build():
         src = patch(open(p).read())
         open(p, "w").write(src)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                        "-DSRBD_PHASE_PROF", "-I", os.path.join(ROOT, "include"), "-o", LIB,
+                        "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), "-I", os.path.join(ROOT, "include"), "-o", LIB,
                         os.path.join(d, "srbd_mpc.hip")], check=True)
 
 
