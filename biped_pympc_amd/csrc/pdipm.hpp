@@ -39,15 +39,18 @@ struct SolverArgs {
   int batch;
   int init_mode;  // 0: iterate from inputs 6..9; 1: x=0, s=max(h,1), z=1, y=y0 (GPU caller init);
                   // 2: x = input 6, s = max(h - G x, 1), z = 1, y = 0 (_ccs init)
-  int only_flagged;  // 1: solve only QPs the fast kernel flagged (mu output == kFallbackBits)
   double y0;
+  // the library's per-device pool for QPs the stage-invariant kernels cannot take: scratch_slots
+  // slots of SolverLayout(kMaxN).total doubles, each guarded by a lock word (0 = free)
+  double* scratch;
+  int* scratch_locks;
+  int scratch_slots;
 };
 
 // iterative-refinement steps per direction in the LDS-resident and general kernels (the register
 // kernels' one step sits at the FP64 floor at N = 10 / 20)
-constexpr int kRefineSteps = 2;
+constexpr int kRefineSteps = 1;
 
-constexpr unsigned long long kFallbackBits = 0x7FF8DEADBEEF5A5Aull;  // quiet NaN with a payload
 
 __device__ inline const double* solver_in(const SolverArgs& a, int i) {
   return a.dev_in ? a.dev_in[i] : a.in[i];
@@ -315,11 +318,12 @@ struct SolverCtx {
       }
       // in-place symmetric sweep of the 12x12 block (78 packed entries over 64 lanes)
       int r0 = 0, r1 = 0;
-      const int e0 = lane, e1 = lane + 64;
+      const int e0 = lane < 64 ? lane : 0, e1 = lane + 64;  // (an idle lane, lane >= 64, stores nothing)
       while ((r0 + 1) * (r0 + 2) / 2 <= e0) ++r0;
       if (e1 < 78)
         while ((r1 + 1) * (r1 + 2) / 2 <= e1) ++r1;
       const int c0 = e0 - r0 * (r0 + 1) / 2, c1 = e1 - r1 * (r1 + 1) / 2;
+      const bool own0 = lane < 64;
       for (int k = 0; k < 12; ++k) {
         const double id = 1.0 / Di[k * (k + 1) / 2 + k];
         const double a0 = Di[e0], k0r = Di[sym_idx(r0, k)], k0c = Di[sym_idx(c0, k)];
@@ -335,11 +339,11 @@ struct SolverCtx {
           else if (r1 == k && c1 == k) n1 = -id;
           else n1 = a1 * id;
         }
-        Di[e0] = n0;
+        if (own0) Di[e0] = n0;
         if (e1 < 78) Di[e1] = n1;
         __syncthreads();
       }
-      Di[e0] = -Di[e0];
+      if (own0) Di[e0] = -Di[e0];
       if (e1 < 78) Di[e1] = -Di[e1];
       __syncthreads();
     }
@@ -618,9 +622,11 @@ struct SolverCtx {
   }
 };
 
-#ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again
-__device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+// The general solve of QP `env` with its working set at `smem` (the workgroup's LDS in pdipm_kernel,
+// a slot of the library's global scratch pool when a stage-invariant kernel meets a QP it cannot
+// take). `lane` >= 64 marks an idle lane (the second wave of a two-wave QP): it takes part in every
+// barrier and stores nothing.
+__device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in) {
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;
@@ -629,7 +635,7 @@ __device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
   C.m = 16 * N;
   C.p = 14 * N;
   C.nd = 12 * N;
-  C.lane = threadIdx.x;
+  C.lane = lane_in;
   C.AV = smem + Lo.AV; C.GV = smem + Lo.GV; C.HV = smem + Lo.HV;
   C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
   C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE;
@@ -738,18 +744,45 @@ __device__ __forceinline__ void pdipm_general(const SolverArgs& args, int env) {
   }
 }
 
-// One workgroup per QP; as the fallback pass behind the stage-invariant kernels (only_flagged) a
-// bounded grid walks the batch and solves just the QPs they flagged (none for qp_former output).
+// A QP the stage-invariant kernels cannot take (not stage-invariant: any CCS input other than
+// qp_former's output), solved inside the same launch by the workgroup that found it, in a slot of
+// the library's scratch pool (global memory, L2-resident): lane 0 takes a free slot by its lock word
+// (a slot holder is a running workgroup that releases it when done, so the spin ends), the solve runs
+// with the slot as its working set, and the slot's writes are released (agent-scope fence) before its
+// lock. Not inlined: the stage-invariant kernels keep their own register allocation; one copy per
+// calling kernel (kTag), so each is compiled under its caller's occupancy target (the register
+// kernels' 2 waves per SIMD). A qp_former batch never gets here, so the fast path pays nothing for
+// it (no second launch, no flag pass).
+// `args` is the kernel's own argument, addressed in the kernarg segment (kernel_args()): taking the
+// address of the by-value kernel parameter instead would copy it to scratch and make the caller
+// read every argument from there.
+__device__ __forceinline__ const SolverArgs& kernel_args() {
+  return *(const SolverArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // constant -> generic address space
+}
+template <int kTag>
+__device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs& args, int env) {
+  const int n = args.scratch_slots;
+  int slot = env % n;
+  if (threadIdx.x == 0) {
+    while (atomicCAS(&args.scratch_locks[slot], 0, 1) != 0) {
+      slot = slot + 1 == n ? 0 : slot + 1;
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  slot = __shfl(slot, 0, 64);  // wave 0's slot (an idle second wave never touches the slot)
+  __threadfence();
+  const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
+  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane);
+  __syncthreads();
+  __threadfence();
+  if (threadIdx.x == 0) atomicExch(&args.scratch_locks[slot], 0);
+}
+
+#ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again
+// One workgroup per QP (the "general" solver path, srbd_set_solver_path(1))
 __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
-  if (!args.only_flagged) {
-    if ((int)blockIdx.x < args.batch) pdipm_general(args, blockIdx.x);
-    return;
-  }
-  for (int env = blockIdx.x; env < args.batch; env += gridDim.x) {
-    if (__double_as_longlong(solver_out(args, 5)[env]) != (long long)kFallbackBits) continue;
-    pdipm_general(args, env);
-    __syncthreads();  // the next flagged QP reuses this workgroup's LDS
-  }
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  if ((int)blockIdx.x < args.batch) pdipm_general_at(args, blockIdx.x, smem, threadIdx.x);
 }
 #endif  // SRBD_NO_GENERAL_KERNEL
 

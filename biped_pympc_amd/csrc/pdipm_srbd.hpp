@@ -14,8 +14,8 @@
 //            the four decoupled u columns)
 // so each iteration only rebuilds the two 4x4 foot blocks of Phi_u per stage. All inner loops have
 // compile-time trip counts over dense 12-wide rows (no pattern tables, no branches).
-// A QP that is not stage-invariant is left to pdipm_kernel: this kernel writes kFallbackMu into its
-// mu output and pdipm_kernel (only_flagged = 1) solves exactly those.
+// A QP that is not stage-invariant is solved by the general algorithm inside the same launch, in a
+// slot of the library's scratch pool (pdipm.hpp pdipm_general_scratch).
 #pragma once
 #include "pdipm.hpp"
 
@@ -782,10 +782,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < 12 * N ? 0 : 12 * N) + e % 12]);
   const bool any_bad = __any(bad);
   if (any_bad) {
-    if (lane == 0) {
-      double* mo = solver_out(args, 5) + (size_t)env;
-      *mo = __longlong_as_double((long long)kFallbackBits);
-    }
+    pdipm_general_scratch<100 + NT>(kernel_args(), env);  // the kernel's sole argument
     return;
   }
   // ---- per-QP constants ----

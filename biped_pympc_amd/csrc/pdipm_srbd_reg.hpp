@@ -1364,8 +1364,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       bad = reinterpret_cast<int*>(smem + Lo::RED)[0] | reinterpret_cast<int*>(smem + Lo::RED)[1];
       qp_sync<TPB>();  // RED is reused by the first block reduction
     }
-    if (bad) {
-      if (lane == 0) solver_out(args, 5)[env] = __longlong_as_double((long long)kFallbackBits);
+    if (bad) {  // not stage-invariant: the general solve, in this launch (pdipm_general_scratch)
+      pdipm_general_scratch<N>(kernel_args(), env);  // the kernel's sole argument
       return;
     }
   }

@@ -34,7 +34,7 @@ int set_error(int code, const char* what) {
 
 constexpr int kFormerWaves = 4;
 constexpr int kErrInvalid = (int)hipErrorInvalidValue;
-constexpr int kFallbackGrid = 512;
+constexpr int kScratchSlots = 256;  // general solves of non-stage-invariant QPs in flight per device
 
 bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 
@@ -78,12 +78,55 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
   return e == hipSuccess ? 0 : set_error((int)e, "qp_former_kernel launch");
 }
 
+// The per-device scratch pool of the stage-invariant solver kernels (pdipm.hpp
+// pdipm_general_scratch): kScratchSlots slots of SolverLayout(kMaxN) doubles (~39 MB) and their lock
+// words, allocated on the first stage-invariant solver call on a device and kept for the process.
+struct ScratchPool {
+  double* buf = nullptr;
+  int* locks = nullptr;
+};
+srbd::PerDevice<ScratchPool> g_scratch;
+std::mutex g_scratch_mu;
+
+int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  ScratchPool* pool = g_scratch.at(dev);
+  if (!pool) return set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
+  if (!pool->buf) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+      return set_error(kErrInvalid, "srbd solver: first call on this device inside a stream capture (the "
+                                    "scratch pool is allocated on first use: call once before capturing)");
+    const size_t per_slot = (size_t)srbd::SolverLayout(srbd::kMaxN).total;
+    double* buf = nullptr;
+    int* locks = nullptr;
+    hipError_t e = hipMalloc(&buf, sizeof(double) * per_slot * kScratchSlots);
+    if (e == hipSuccess) e = hipMalloc(&locks, sizeof(int) * kScratchSlots);
+    if (e == hipSuccess) e = hipMemset(locks, 0, sizeof(int) * kScratchSlots);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      (void)hipFree(buf);
+      (void)hipFree(locks);
+      return set_error((int)e, "srbd solver: scratch pool allocation");
+    }
+    pool->buf = buf;
+    pool->locks = locks;
+  }
+  a.scratch = pool->buf;
+  a.scratch_locks = pool->locks;
+  a.scratch_slots = kScratchSlots;
+  return 0;
+}
+
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
   static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20, cfg_reg10, cfg_reg20;
   srbd::SolverArgs a = a0;
-  a.only_flagged = 0;
   const int path = solver_path();
+  // the stage-invariant kernels solve any other QP of the batch in the same launch (scratch pool)
+  if (path != 1)
+    if (int rc = attach_scratch(a, s)) return rc;
   if (path == 0 && (a.N == 10 || a.N == 20)) {
     if (a.N == 10) {
       if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, cfg_reg10)) return rc;
@@ -98,9 +141,9 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
 #endif
     }
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_reg_kernel launch");
-    a.only_flagged = 1;
-  } else if (path == 0 || path == 2) {
+    return e == hipSuccess ? 0 : set_error((int)e, "pdipm_srbd_reg_kernel launch");
+  }
+  if (path == 0 || path == 2) {
     const size_t lds = fast_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
     // horizon-specialised instantiations for the common horizons, runtime-N otherwise
@@ -113,16 +156,12 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
     else if (a.N == 20) hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<20>, dim3(a.batch), dim3(64), lds, s, a);
     else hipLaunchKernelGGL(srbd::pdipm_srbd_kernel<0>, dim3(a.batch), dim3(64), lds, s, a);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_error((int)e, "pdipm_srbd_kernel launch");
-    a.only_flagged = 1;  // general kernel picks up the QPs that are not stage-invariant
+    return e == hipSuccess ? 0 : set_error((int)e, "pdipm_srbd_kernel launch");
   }
   const size_t lds = solver_lds_bytes(a.N);
   if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
   if (int rc = ensure_lds_attr((const void*)srbd::pdipm_kernel, lds, cfg_general)) return rc;
-  // the fallback pass walks the batch with a bounded grid and solves only the flagged QPs (none for
-  // qp_former output): a few hundred short workgroups instead of one large-LDS workgroup per QP
-  const int grid = a.only_flagged ? (a.batch < kFallbackGrid ? a.batch : kFallbackGrid) : a.batch;
-  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(grid), dim3(64), lds, s, a);
+  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(64), lds, s, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "pdipm_kernel launch");
 }
