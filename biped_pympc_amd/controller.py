@@ -6,15 +6,14 @@ Mirrors the reference controller API so a user of ``MPCControllerCusadi`` can sw
   * ``BaseMPCController`` setters and knot-point state (``convex_mpc/base_controller.py:11-266``),
   * ``MPCControllerHIP.run() -> (foot_wrench (B,2,6) float32, cost (B,))`` with the semantics of
     ``MPCControllerCusadi.run`` (``convex_mpc/mpc_controller_cusadi.py:43-205``).
-At N = 10 and 20 the whole step is ONE kernel launch on the caller's current HIP stream with no
+At every horizon the whole step is ONE kernel launch on the caller's current HIP stream with no
 host synchronisation (``srbd_mpc_step``): the input preparation (knot points, initial state,
 reference trajectory, contact schedule, I_world -- the ~40 small FP32 torch ops of the reference)
 into on-chip memory, the fused former + PDIPM (cold start, ``cfg.pdipm_iterations`` Newton
 iterations; the reference runs a former call and 4 solver calls x 5 iterations with host round
 trips) and the u0 -> wrench (-> stance torque) epilogue; only the (B, 2, 6) wrench leaves the chip
-unless ``cfg.keep_solution``. Other horizons run the same three stages as three kernels
-(``run_three_kernel``, bit-identical at N = 10 / 20). ``GraphedMPCStep`` replays the step as a
-captured HIP graph. Nothing of the step is computed in PyTorch; it only owns the buffers.
+unless ``cfg.keep_solution``. ``run_three_kernel`` runs the same three stages as three kernels
+(bit-identical). ``GraphedMPCStep`` replays the step as a captured HIP graph. Nothing of the step is computed in PyTorch; it only owns the buffers.
 
 ``literal_layout=True`` (default) reproduces the reference GPU caller's flattening quirks
 (row-major R_body read column-major, row-major contact table read column-major, a 13-wide Q read
@@ -269,16 +268,14 @@ class MPCControllerHIP(BaseMPCController):
 
     def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """MPCControllerCusadi.run (mpc_controller_cusadi.py:43-205): (foot_wrench (B,2,6) f32, cost)."""
-        if self.horizon_length not in (10, 20):
-            return self.run_three_kernel()
         keep: list = []
         self._step(self._prep_struct(keep), None, None)
         return self.foot_wrench, self.cost
 
     def run_three_kernel(self, J: torch.Tensor | None = None, cb: torch.Tensor | None = None):
         """The same step as three launches (srbd_prepare_inputs -> srbd_mpc_solve_fused ->
-        srbd_u0_wrench_torque) with the 17 former inputs and the solution in device memory; any
-        horizon. Bit-identical to run() at N = 10 / 20 (tests/test_controller.py)."""
+        srbd_u0_wrench_torque) with the 17 former inputs and the solution in device memory.
+        Bit-identical to run() (tests/test_controller.py)."""
         N, B = self.horizon_length, self.num_envs
         self.prepare()
         out = solver.mpc_solve(self.former_inputs, N, self.cfg.pdipm_iterations, self.cfg.y0, self.buffers)
@@ -310,8 +307,6 @@ class MPCControllerHIP(BaseMPCController):
         step's epilogue: tau (B,2,ndof) float32 = J[:,l]^T wrench[:,l] on stance legs, 0 on swing
         legs. contact_jacobian (B,2,6,ndof) float32 (LegControllerData.J), contact_bool (B,2)."""
         J, cb = self._torque_args(contact_jacobian, contact_bool)
-        if self.horizon_length not in (10, 20):
-            return self.run_three_kernel(J, cb)
         keep: list = []
         self._step(self._prep_struct(keep), J, cb)
         return self.foot_wrench, self.cost, self.tau
@@ -322,8 +317,8 @@ MPCControllerCusadi = MPCControllerHIP
 
 
 class GraphedMPCStep:
-    """The controller step captured once as a HIP graph and replayed (one graph launch per step;
-    at N = 10 / 20 the graph holds the single srbd_mpc_step kernel). Worth it when the batch is
+    """The controller step captured once as a HIP graph and replayed (one graph launch per step; the
+    graph holds the single srbd_mpc_step kernel). Worth it when the batch is
     small and launch overhead is a visible share of the step.
 
     The graph records device pointers, so the state / command / schedule tensors must be contiguous
@@ -359,18 +354,7 @@ class GraphedMPCStep:
             self._launch()
 
     def _launch(self) -> None:
-        c, N = self.c, self.c.horizon_length
-        if N in (10, 20):
-            c._step(self._prep, None, None)
-            return
-        L = _native.lib()
-        _native.check(L.srbd_prepare_inputs(N, c.num_envs, ctypes.byref(self._prep),
-                                            _native.ptr_array([t.data_ptr() for t in c.former_inputs]),
-                                            solver._stream_ptr()), "srbd_prepare_inputs")
-        out = solver.mpc_solve(c.former_inputs, N, c.cfg.pdipm_iterations, c.cfg.y0, c.buffers)
-        c.solution = out if c.cfg.keep_solution else None
-        _native.check(L.srbd_u0_wrench(N, c.num_envs, out[0].data_ptr(), self._prep.rotation_body,
-                                       c.foot_wrench.data_ptr(), solver._stream_ptr()), "srbd_u0_wrench")
+        self.c._step(self._prep, None, None)
 
     def _current_signature(self) -> tuple:
         """(name, storage pointer) of every tensor the step reads or updates, plus the constants the

@@ -22,10 +22,13 @@
 namespace srbd {
 
 
+// fused = true (mpc_step_lds_kernel, the one-launch step at any horizon) adds the QP's vectors f, h,
+// b (FV, HV, BV: computed in the prologue, read every iteration), the refinement's saved dx / dy
+// (XS, YS: the CCS kernel parks them in its x / y output rows) and the 17 former inputs (FI).
 struct FastLayout {
   int Md, Nd, Cd, Gd, K0, K1, Pd, IX, Hu, SG, PH, DV, X, S, Z, Y, RX, RS, RE, WD, DI, VV, R2, TV, QV, WV,
-      DS, DZ, DY, SC, total;
-  __host__ __device__ FastLayout(int N) {
+      DS, DZ, DY, SC, FV, HV, BV, XS, YS, FI, total;
+  __host__ __device__ FastLayout(int N, bool fused = false) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
     int o = 0;
     auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };
@@ -38,6 +41,11 @@ struct FastLayout {
     TV = take(nz); QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
     SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector
+    FV = HV = BV = XS = YS = FI = -1;
+    if (fused) {
+      FV = take(nz); HV = take(m); BV = take(p); XS = take(nz); YS = take(p);
+      FI = take(72 + 38 * N);  // former_in_nnz summed over the 17 inputs
+    }
     total = o;
   }
 };
@@ -696,11 +704,11 @@ struct FastCtx {
   }
 
   // kRefineSteps steps of iterative refinement of the direction just solved (affine or combined).
-  // Each step after the first restores the original right-hand side (residuals(): r_x, r_s, r_e;
-  // r2 stays in R2) and takes the full dy = saved + correction, so the next refine_rhs measures the
-  // residual of the ORIGINAL system at the refined direction. One step leaves the longer horizons
-  // (N = 32: 20x the FP64 floor at K = 1) and N = 1 on the general kernel above the floor; two reach
-  // it (tests/test_gpu_parity.py::test_runtime_horizon_solver_matches_oracle).
+  // A step after the first restores the original right-hand side (residuals(): r_x, r_s, r_e; r2
+  // stays in R2) and takes the full dy = saved + correction, so its refine_rhs measures the residual
+  // of the ORIGINAL system at the refined direction. One step per direction reaches the FP64 floor
+  // once the affine direction is refined too (profiles/r03/runtime_parity_probe.txt); a second one
+  // moves nothing.
   __device__ void refine() {
     const int N = NT > 0 ? NT : N_, p = 14 * N;
     for (int step = 0; step < kRefineSteps; ++step) {
@@ -711,6 +719,105 @@ struct FastCtx {
       refine_rhs();
       solve(2, 0.0);
     }
+  }
+
+  __device__ void bind(double* smem, const FastLayout& Lo) {
+    Md = smem + Lo.Md; Nd = smem + Lo.Nd; Cd = smem + Lo.Cd; Gd = smem + Lo.Gd;
+    K0 = smem + Lo.K0; K1 = smem + Lo.K1; Pd = smem + Lo.Pd; IX = smem + Lo.IX;
+    Hu = smem + Lo.Hu; SG = smem + Lo.SG; PH = smem + Lo.PH; DV = smem + Lo.DV;
+    X = smem + Lo.X; S = smem + Lo.S; Z = smem + Lo.Z; Y = smem + Lo.Y;
+    RX = smem + Lo.RX; RS = smem + Lo.RS; RE = smem + Lo.RE; WD = smem + Lo.WD; DI = smem + Lo.DI;
+    VV = smem + Lo.VV; R2 = smem + Lo.R2; TV = smem + Lo.TV; QV = smem + Lo.QV; WV = smem + Lo.WV;
+    DS = smem + Lo.DS; DZ = smem + Lo.DZ; DY = smem + Lo.DY; SC = smem + Lo.SC;
+  }
+
+  // per-QP constants from the stage blocks Md / Nd / Pd / Hu (and the x-moment coefficients e6, e9,
+  // valid on lane 0): IX, SG, the coupling block C = M diag(P / phi_x) and the constant parts K0 /
+  // K1 of the diagonal dual blocks
+  __device__ void constants(double e6, double e9) {
+    if (lane < 12) IX[lane] = 1.0 / (Hu[12 + lane] + kBeta);
+    if (lane == 0) {
+      const double p6 = Hu[6] + kBeta, p9 = Hu[9] + kBeta;
+      SG[0] = kDelta / (p6 * kDelta + e6 * e6);
+      SG[1] = 1.0 / (Hu[8] + kBeta);
+      SG[2] = kDelta / (p9 * kDelta + e9 * e9);
+      SG[3] = 1.0 / (Hu[11] + kBeta);
+      SG[4] = p6;
+      SG[5] = p9;
+      SG[6] = e6;
+      SG[7] = e9;
+    }
+    __syncthreads();
+    for (int e = lane; e < 144; e += 64) {
+      const int j = e % 12;
+      Cd[e] = Md[e] * (Pd[j] * IX[j]);
+    }
+    for (int e = lane; e < 78; e += 64) {
+      int r, c;
+      tri_rc(e, r, c);
+      double k0 = (r == c) ? Pd[r] * Pd[r] * IX[r] + kDelta : 0.0;
+      k0 += Nd[r * 12 + 6] * Nd[c * 12 + 6] * SG[0] + Nd[r * 12 + 8] * Nd[c * 12 + 8] * SG[1] +
+            Nd[r * 12 + 9] * Nd[c * 12 + 9] * SG[2] + Nd[r * 12 + 11] * Nd[c * 12 + 11] * SG[3];
+      double k1 = k0;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) k1 += Md[r * 12 + j] * Md[c * 12 + j] * IX[j];
+      K0[e] = k0;
+      K1[e] = k1;
+    }
+  }
+
+  // n_iter Mehrotra iterations from the iterate in X, S, Z, Y (sparse_pdipm_solver.py:376-521);
+  // res = the last iteration's pre-update residual norms [|rx|, |rs|, |re|] and mu_new (:523-530)
+  __device__ void newton(int n_iter, double (&res)[4]) {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    double mu_new = 0.0;
+    for (int it = 0; it < n_iter; ++it) {
+      const double mu = residuals();
+      if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
+        double a = 0.0, b = 0.0, c = 0.0;
+        for (int e = lane; e < nz; e += 64) a += RX[e] * RX[e];
+        for (int e = lane; e < m; e += 64) b += RS[e] * RS[e];
+        for (int e = lane; e < p; e += 64) c += RE[e] * RE[e];
+        res[0] = sqrt(wave_sum(a));
+        res[1] = sqrt(wave_sum(b));
+        res[2] = sqrt(wave_sum(c));
+      }
+      // The affine direction is refined too: its ds, dz enter sigma and the corrector's right-hand
+      // side, which the combined direction's refinement cannot correct. The register kernels refine
+      // it only at degenerate iterates (an s at its clamp, W = z / s ~ 1e8); this kernel serves the
+      // longer horizons, where the unrefined affine direction already leaves K = 1 at 25x the FP64
+      // floor (N = 32, scripts/runtime_parity_probe.py), so it refines it in every iteration.
+      PROF_ADD(0);
+      factor();
+      solve(0, 0.0);
+      refine();
+      residuals();  // restores r_x, r_s, r_e for the combined solve
+      const double ap = step_length(S, DS), ad = step_length(Z, DZ);
+      double sza = 0.0;
+      for (int q = lane; q < m; q += 64) sza += (S[q] + ap * DS[q]) * (Z[q] + ad * DZ[q]);
+      const double mu_aff = wave_sum(sza) / m;
+      const double sigma = pow(mu_aff / mu, 3.0);
+      __syncthreads();
+      PROF_ADD(5);
+      solve(1, sigma * mu * 1.0);
+      refine();
+      const double apc = step_length(S, DS), adc = step_length(Z, DZ);
+      __syncthreads();
+      double szn = 0.0;
+      for (int e = lane; e < nz; e += 64) X[e] = X[e] + apc * TV[e];
+      for (int q = lane; q < m; q += 64) {
+        const double sn = fmax(S[q] + apc * DS[q], 1e-8);
+        const double zn = fmax(fmax(Z[q] + adc * DZ[q], 1e-8), 1e-8);
+        S[q] = sn;
+        Z[q] = zn;
+        szn += sn * zn;
+      }
+      for (int e = lane; e < p; e += 64) Y[e] = Y[e] + adc * (ysg[e] + DY[e]);  // saved + correction
+      mu_new = wave_sum(szn) / m;
+      __syncthreads();
+      PROF_ADD(5);
+    }
+    res[3] = mu_new;
   }
 
   __device__ double step_length(const double* v, const double* dv) const {
@@ -737,13 +844,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   FastCtx<NT> C;
   C.N_ = N;
   C.lane = lane;
-  C.Md = smem + Lo.Md; C.Nd = smem + Lo.Nd; C.Cd = smem + Lo.Cd; C.Gd = smem + Lo.Gd;
-  C.K0 = smem + Lo.K0; C.K1 = smem + Lo.K1; C.Pd = smem + Lo.Pd; C.IX = smem + Lo.IX;
-  C.Hu = smem + Lo.Hu; C.SG = smem + Lo.SG; C.PH = smem + Lo.PH; C.DV = smem + Lo.DV;
-  C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
-  C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE; C.WD = smem + Lo.WD; C.DI = smem + Lo.DI;
-  C.VV = smem + Lo.VV; C.R2 = smem + Lo.R2; C.TV = smem + Lo.TV; C.QV = smem + Lo.QV; C.WV = smem + Lo.WV;
-  C.DS = smem + Lo.DS; C.DZ = smem + Lo.DZ; C.DY = smem + Lo.DY; C.SC = smem + Lo.SC;
+  C.bind(smem, Lo);
   const int nz = 24 * N, m = 16 * N, p = 14 * N, nA = nnz_A(N), nG = 28 * N;
   const double* Hg = solver_in(args, 0) + (size_t)env * nz;
   const double* Gg = solver_in(args, 1) + (size_t)env * nG;
@@ -786,36 +887,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
     return;
   }
   // ---- per-QP constants ----
-  if (lane < 12) C.IX[lane] = 1.0 / (C.Hu[12 + lane] + kBeta);
-  if (lane == 0) {
-    const double e6 = Ag[a_ubase(N) + c_tab.e6], e9 = Ag[a_ubase(N) + c_tab.e9];
-    const double p6 = C.Hu[6] + kBeta, p9 = C.Hu[9] + kBeta;
-    C.SG[0] = kDelta / (p6 * kDelta + e6 * e6);
-    C.SG[1] = 1.0 / (C.Hu[8] + kBeta);
-    C.SG[2] = kDelta / (p9 * kDelta + e9 * e9);
-    C.SG[3] = 1.0 / (C.Hu[11] + kBeta);
-    C.SG[4] = p6;
-    C.SG[5] = p9;
-    C.SG[6] = e6;
-    C.SG[7] = e9;
-  }
-  __syncthreads();
-  for (int e = lane; e < 144; e += 64) {
-    const int r = e / 12, j = e % 12;
-    C.Cd[e] = C.Md[e] * (C.Pd[j] * C.IX[j]);
-  }
-  for (int e = lane; e < 78; e += 64) {
-    int r, c;
-    tri_rc(e, r, c);
-    double k0 = (r == c) ? C.Pd[r] * C.Pd[r] * C.IX[r] + kDelta : 0.0;
-    k0 += C.Nd[r * 12 + 6] * C.Nd[c * 12 + 6] * C.SG[0] + C.Nd[r * 12 + 8] * C.Nd[c * 12 + 8] * C.SG[1] +
-          C.Nd[r * 12 + 9] * C.Nd[c * 12 + 9] * C.SG[2] + C.Nd[r * 12 + 11] * C.Nd[c * 12 + 11] * C.SG[3];
-    double k1 = k0;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) k1 += C.Md[r * 12 + j] * C.Md[c * 12 + j] * C.IX[j];
-    C.K0[e] = k0;
-    C.K1[e] = k1;
-  }
+  C.constants(Ag[a_ubase(N) + c_tab.e6], Ag[a_ubase(N) + c_tab.e9]);
   // ---- iterate ----
   if (args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
@@ -838,54 +910,9 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   }
   __syncthreads();
 
-  double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
+  double res[4] = {0.0, 0.0, 0.0, 0.0};
   PROF_MARK_CTX(C);
-  for (int it = 0; it < args.n_iter; ++it) {
-    const double mu = C.residuals();
-    if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
-      double a = 0.0, b = 0.0, c = 0.0;
-      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
-      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
-      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
-      res0 = sqrt(wave_sum(a));
-      res1 = sqrt(wave_sum(b));
-      res2 = sqrt(wave_sum(c));
-    }
-    // The affine direction is refined too: its ds, dz enter sigma and the corrector's right-hand
-    // side, which the combined direction's refinement cannot correct. The register kernels refine it
-    // only at degenerate iterates (an s at its clamp, W = z / s ~ 1e8); this kernel serves the
-    // longer horizons, where the unrefined affine direction already leaves K = 1 at 25x the FP64
-    // floor (N = 32, scripts/runtime_parity_probe.py), so it refines it in every iteration.
-    PROF_ADD_CTX(C, 0);
-    C.factor();
-    C.solve(0, 0.0);
-    C.refine();
-    C.residuals();  // restores r_x, r_s, r_e for the combined solve
-    const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
-    double sza = 0.0;
-    for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
-    const double mu_aff = wave_sum(sza) / m;
-    const double sigma = pow(mu_aff / mu, 3.0);
-    __syncthreads();
-    PROF_ADD_CTX(C, 5);
-    C.solve(1, sigma * mu * 1.0);
-    C.refine();
-    const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
-    __syncthreads();
-    double szn = 0.0;
-    for (int e = lane; e < nz; e += 64) C.X[e] = C.X[e] + apc * C.TV[e];
-    for (int q = lane; q < m; q += 64) {
-      const double sn = fmax(C.S[q] + apc * C.DS[q], 1e-8);
-      const double zn = fmax(fmax(C.Z[q] + adc * C.DZ[q], 1e-8), 1e-8);
-      C.S[q] = sn;
-      C.Z[q] = zn;
-      szn += sn * zn;
-    }
-    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
-    mu_new = wave_sum(szn) / m;
-    __syncthreads();
-    PROF_ADD_CTX(C, 5);
-  }
+  C.newton(args.n_iter, res);
   PROF_FLUSH(C);
   double* xo = solver_out(args, 0) + (size_t)env * nz;
   double* so = solver_out(args, 1) + (size_t)env * m;
@@ -897,11 +924,9 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   for (int e = lane; e < m; e += 64) { so[e] = C.S[e]; zo[e] = C.Z[e]; }
   for (int e = lane; e < p; e += 64) yo[e] = C.Y[e];
   if (lane == 0) {
-    ro[0] = res0;
-    ro[1] = res1;
-    ro[2] = res2;
-    ro[3] = mu_new;
-    mo[0] = mu_new;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ro[k] = res[k];
+    mo[0] = res[3];
   }
 }
 

@@ -48,9 +48,10 @@ struct Tables {
   // row -1 = the +I entry of an x column, row 12/13 = the x-moment entries e6/e9 of a u block.
   int8_t xb_r[36], xb_j[36];
   int8_t ub_r[86], ub_j[86];
-  // Packed-lower 12x12 entries (row | col << 4, row >= col) sorted for the S_ii build: rows/cols
-  // {0,1,2,6,7,8} meet every foot column of N ("dense"), rows {3,4,5,9,10,11} exactly one per foot
-  // (position r % 3). Order: 21 dense-dense, 36 sparse-dense, 21 sparse-sparse.
+  // Packed-lower 12x12 entries (row | col << 4, row >= col) in the lane order of the S_ii build:
+  // rows/cols {0,1,2,6,7,8} meet every foot column of N ("dense"), rows {3,4,5,9,10,11} exactly one
+  // per foot (position r % 3). 21 dense-dense entries, then the 57 with a sparse index; within each
+  // class the order minimises the bank conflicts of the entries' LDS stores (kSiiOrder).
   uint8_t dvo[78];
   // Foot blocks of Phi_u: u columns {0,1,2,7} (left) and {3,4,5,10} (right).
   int8_t foot_col[2][4];
@@ -58,6 +59,15 @@ struct Tables {
   int8_t col_foot[12];
   int8_t col_pos[12];
 };
+
+// kSiiOrder: scripts/sii_order.py (a seeded search over the order within each class: the extra
+// LDS cycles of a stage block's ds_write_b64 fall from 6 to 5 (dense pass) and 4 to 1 (sparse pass)
+// per instruction against the class-sorted row-major order; tests/test_layout.py checks the classes)
+constexpr uint8_t kSiiOrder[78] = {120, 0,   23,  38,  24,  103, 17,  136, 104, 7,   102, 18,  40,  119, 22,  1,
+                                   34,  2,   8,   6,   39,  20,  58,  68,  86,  85,  35,  37,  91,  56,  71,  88,
+                                   121, 9,   107, 25,  3,   57,  75,  52,  139, 69,  154, 106, 170, 51,  171, 73,
+                                   11,  55,  72,  123, 187, 53,  74,  137, 36,  10,  41,  70,  89,  21,  155, 105,
+                                   54,  27,  59,  90,  43,  87,  26,  153, 4,   19,  42,  5,   138, 122};
 
 constexpr Tables make_tables() {
   Tables t{};
@@ -147,15 +157,7 @@ constexpr Tables make_tables() {
     t.gr_col[k][t.gr_n[k]] = t.gcol[q];
     t.gr_n[k]++;
   }
-  {
-    int o = 0;
-    for (int cls = 0; cls < 3; ++cls)
-      for (int r = 0; r < 12; ++r)
-        for (int c = 0; c <= r; ++c) {
-          const int sparse = (r % 6 >= 3) + (c % 6 >= 3);
-          if (sparse == cls) t.dvo[o++] = (uint8_t)(r | (c << 4));
-        }
-  }
+  for (int o = 0; o < 78; ++o) t.dvo[o] = kSiiOrder[o];
   const int8_t fl[4] = {0, 1, 2, 7}, fr[4] = {3, 4, 5, 10};
   for (int q = 0; q < 4; ++q) {
     t.foot_col[0][q] = fl[q];

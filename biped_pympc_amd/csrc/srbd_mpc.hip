@@ -15,6 +15,7 @@
 #include "pdipm.hpp"
 #include "pdipm_srbd.hpp"
 #include "pdipm_srbd_reg.hpp"
+#include "mpc_step_lds.hpp"
 #include "qp_former.hpp"
 #include "mpc_io.hpp"
 #include "reg20.hpp"
@@ -334,10 +335,16 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
   return srbd_pdipm_cold(horizon, n_iter, batch, y0, sin, outputs, stream);
 }
 
-// launch of the fused / controller-step kernel (a fully set up FusedArgs)
+// launch of the fused / controller-step kernel (a fully set up FusedArgs): the register kernels at
+// N = 10 and 20, the LDS-resident one-launch step (mpc_step_lds.hpp) at every other horizon
 static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
-  static srbd::LdsAttr cfg10, cfg20;
-  if (a.N == 10) {
+  static srbd::LdsAttr cfg10, cfg20, cfg_lds;
+  if (a.N != 10 && a.N != 20) {
+    const size_t lds = srbd::step_lds_bytes(a.N);
+    if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the one-launch step");
+    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_lds_kernel<0>, lds, cfg_lds)) return rc;
+    hipLaunchKernelGGL(srbd::mpc_step_lds_kernel<0>, dim3(a.batch), dim3(64), lds, st, a);
+  } else if (a.N == 10) {
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, cfg10)) return rc;
     hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, st, a);
   } else {
@@ -355,8 +362,9 @@ static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
 
 int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                          double* qp_workspace, double* const* outputs, void* stream) {
-  if (!(horizon == 10 || horizon == 20) || solver_path() != 0) {  // no fused kernel: former + solver
-    if (!qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve_fused: this horizon / solver path needs qp_workspace");
+  if (!horizon_ok(horizon)) return set_error(kErrInvalid, "srbd_mpc_solve_fused: bad horizon");
+  if (solver_path() != 0) {  // a non-auto solver path: former + that solver kernel
+    if (!qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve_fused: a non-auto solver path needs qp_workspace");
     return srbd_mpc_solve(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, stream);
   }
   if (n_iter < 1 || batch < 0 || !former_inputs || !outputs)
@@ -425,9 +433,7 @@ static int fill_prep(const srbd_mpc_prep* p, srbd::PrepArgs& a, const char* who)
 int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
                   double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
                   const float* contact_jacobian, const float* contact_bool, float* tau, void* stream) {
-  if (!(horizon == 10 || horizon == 20))
-    return set_error(kErrInvalid, "srbd_mpc_step: horizon 10 or 20 (other horizons: srbd_prepare_inputs + "
-                                  "srbd_mpc_solve + srbd_u0_wrench_torque)");
+  if (!horizon_ok(horizon)) return set_error(kErrInvalid, "srbd_mpc_step: bad horizon");
   if (n_iter < 1 || batch < 0 || !prep || (tau && (ndof < 1 || ndof > 64)))
     return set_error(kErrInvalid, "srbd_mpc_step: bad arguments");
   if (batch == 0) return 0;

@@ -129,10 +129,11 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
 
     Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
     iteration count as a runtime argument. Returns [x, s, z, y, residuals, mu].
-    ``fused`` (default): for N = 10 and 20 one kernel forms the QP in registers / LDS and solves it
-    (``srbd_mpc_solve_fused``): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to
-    their ``buffers.workspace`` slots); ``False`` runs the former and the solver as two kernels
-    with the full QP in the workspace.
+    ``fused`` (default): one kernel forms the QP in registers / LDS and solves it
+    (``srbd_mpc_solve_fused``; the register kernels at N = 10 and 20, the LDS-resident step kernel at
+    other horizons): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to their
+    ``buffers.workspace`` slots); ``False`` runs the former and the solver as two kernels with the
+    full QP in the workspace. Both give the same bits.
     """
     d = Dims(N)
     B = former_inputs[0].shape[0]
@@ -143,9 +144,9 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     if buffers.workspace.device != former_inputs[0].device:
         raise ValueError(f"mpc_solve: workspace on {buffers.workspace.device}, inputs on {former_inputs[0].device}")
     L = _native.lib()
-    # the fused kernel runs only at N = 10 / 20 under the auto solver path; otherwise the former
-    # writes the whole QP into the workspace for the solver kernel
-    one_kernel = fused and N in (10, 20) and _native.current_solver_path() == 0
+    # the fused kernel runs under the auto solver path (any horizon); otherwise the former writes the
+    # whole QP into the workspace for the solver kernel
+    one_kernel = fused and _native.current_solver_path() == 0
     rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
                           _native.ptr_array([t.data_ptr() for t in former_inputs]),
                           buffers.workspace.data_ptr() if (keep_qp or not one_kernel) else None,

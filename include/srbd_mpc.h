@@ -80,11 +80,12 @@ size_t srbd_mpc_workspace_doubles(int horizon, int batch);
 int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                    double* qp_workspace, double* const* outputs, void* stream);
 
-/* srbd_mpc_solve in ONE kernel for N = 10 and 20 (other horizons, or a non-auto solver path, run
- * srbd_mpc_solve and need qp_workspace): the QP is formed in the solver from the former inputs and
- * never written, except f, b, d into their qp_workspace slots when qp_workspace != NULL (NULL: no
- * QP data leaves the kernel). Same outputs as srbd_mpc_solve; any outputs[k] may be NULL (that
- * output is not written). */
+/* srbd_mpc_solve in ONE kernel at every horizon (the register kernels at N = 10 and 20, the
+ * LDS-resident step kernel otherwise; a non-auto solver path runs srbd_mpc_solve and needs
+ * qp_workspace): the QP is formed in the solver from the former inputs and never written, except
+ * f, b, d into their qp_workspace slots when qp_workspace != NULL (NULL: no QP data leaves the
+ * kernel). Same outputs as srbd_mpc_solve, bit for bit; any outputs[k] may be NULL (that output is
+ * not written). */
 int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                          double* qp_workspace, double* const* outputs, void* stream);
 
@@ -158,7 +159,7 @@ typedef struct srbd_mpc_prep {
 int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* prep, double* const* former_inputs,
                         void* stream);
 
-/* The whole controller step in ONE kernel launch (N = 10 and 20): srbd_prepare_inputs' arithmetic
+/* The whole controller step in ONE kernel launch (any horizon 1..32): srbd_prepare_inputs' arithmetic
  * computes this env's 17 former inputs into on-chip memory (and advances the knot-point state in
  * prep), the fused former + cold PDIPM (n_iter iterations, y = y0) solves, and
  * srbd_u0_wrench_torque's arithmetic writes foot_wrench (B,2,6) float32 -- and tau (B,2,ndof) when

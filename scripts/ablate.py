@@ -114,11 +114,12 @@ VARIANTS = {
     "fchain2": lambda s: s.replace("    C.template factor_chain<true>();  // + the affine forward elimination",
                                    "    C.template factor_chain<true>();\n    C.template factor_chain<true>();"),
     # the combined solve's right-hand side twice (idempotent)
-    "rhs2": lambda s: s.replace("    solve_rhs<kMode>(smu);\n    solve_chain<false>();",
-                                "    solve_rhs<kMode>(smu);\n    solve_rhs<kMode>(smu);\n    solve_chain<false>();"),
+    "rhs2": lambda s: s.replace("    solve_rhs<kMode>(smu, rx);\n    solve_chain<false>();",
+                                "    solve_rhs<kMode>(smu, rx);\n    solve_rhs<kMode>(smu, rx);\n    solve_chain<false>();"),
     # the combined solve's finish twice (cost only)
-    "finish2": lambda s: s.replace("    solve_chain<false>();\n    solve_finish<false>();",
-                                   "    solve_chain<false>();\n    solve_finish<false>();\n    solve_finish<false>();"),
+    "finish2": lambda s: s.replace("    solve_chain<false>();\n    solve_finish<false, false, true>();",
+                                   "    solve_chain<false>();\n    solve_finish<false, false, true>();\n"
+                                   "    solve_finish<false, false, true>();"),
     # odd workgroups start their Newton loop ~40k cycles late (5 x s_sleep 127), so the two waves
     # sharing a SIMD tend to sit in different phases (chain vs row-parallel) -- a phase-offset probe
     "stagger": lambda s: s.replace("  PROF_MARK_CTX(C);\n",

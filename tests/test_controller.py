@@ -248,8 +248,8 @@ def test_dense_scatter_matches_layout(which):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K", [20, 30])
-def test_controller_step_matches_oracle_pipeline(K):
+@pytest.mark.parametrize("N,K", [(10, 20), (10, 30), (5, 20), (32, 20), (1, 30)])
+def test_controller_step_matches_oracle_pipeline(N, K):
     """prepare -> fused former + K-iteration PDIPM -> wrench against the oracle pipeline.
 
     K = 20 is the controller default (the reference's 4 x 5 schedule). Every env must meet
@@ -257,7 +257,7 @@ def test_controller_step_matches_oracle_pipeline(K):
     FP32, so errors are relative to max(|wrench|, 1 N).
     """
     from oracle import oracle
-    N, B = 10, 128
+    B = 128
     st, cmd, ctrl, params, gait_args, table = random_robot(B, 21, N, gait=True)
     c = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
     c.cfg.pdipm_iterations = K
@@ -268,8 +268,20 @@ def test_controller_step_matches_oracle_pipeline(K):
     ref = mpc_io.u0_wrench(N, x, st["rotation_body"])
     w = wrench.cpu().numpy()
     assert w.shape == (B, 2, 6) and w.dtype == np.float32 and cost.shape == (B,)
-    err = np.abs(w - ref).max(axis=(1, 2)) / np.maximum(np.abs(ref).max(axis=(1, 2)), 1.0)
-    assert err.max() <= (1e-6 if K >= 30 else 1e-4), np.sort(err)[-8:]
+    rel = lambda a, r: np.abs(a - r).max(axis=(1, 2)) / np.maximum(np.abs(r).max(axis=(1, 2)), 1.0)
+    err = rel(w, ref)
+    bar = 1e-6 if K >= 30 else 1e-4
+    # an env above the bar must sit within 4x of its FP64 floor: the distance between the oracle
+    # (sparse LDL^T) and the independent dense-LU restatement of the same solve (one N = 1 env's
+    # two CPU solutions differ by 2.4e-4 in the wrench at K = 30)
+    from oracle.pdipm_dense import pdipm_dense
+    from biped_pympc_amd.utils.synthetic import solver_init
+    H, f, A, b, G, d = oracle.qp_former(N, ins)
+    it = solver_init(d, N, y0=1.0)
+    for e in np.flatnonzero(err > bar):
+        xd = pdipm_dense(N, K, H[e], G[e], A[e], f[e], d[e], b[e], *(t[e] for t in it))[0]
+        floor = rel(mpc_io.u0_wrench(N, xd[None], st["rotation_body"][e:e + 1]), ref[e:e + 1])[0]
+        assert err[e] <= 4.0 * floor, (e, err[e], floor)
 
 
 @pytest.mark.gpu
@@ -288,11 +300,12 @@ def test_controller_run_with_torque():
 
 
 @pytest.mark.gpu
-def test_graphed_step_replays_the_controller_step():
+@pytest.mark.parametrize("N", [10, 5])
+def test_graphed_step_replays_the_controller_step(N):
     """GraphedMPCStep: one captured graph launch per step, same wrench as run(), and replays pick
-    up state updated in place."""
+    up state updated in place (N = 5: the LDS-resident one-launch step)."""
     from biped_pympc_amd.controller import GraphedMPCStep
-    N, B = 10, 64
+    B = 64
     st, cmd, ctrl, params, gait_args, table = random_robot(B, 31, N, gait=True)
     c1 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
     c2 = _controller(B, N, st, cmd, ctrl, params, gait_args, table)
@@ -310,7 +323,9 @@ def test_graphed_step_replays_the_controller_step():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,gait,literal,torque", [(10, True, True, False), (10, False, True, True),
-                                                   (20, True, False, True), (10, True, True, True)])
+                                                   (20, True, False, True), (10, True, True, True),
+                                                   (5, True, True, True), (32, False, False, False),
+                                                   (1, True, True, False)])
 def test_one_launch_step_equals_three_kernels(N, gait, literal, torque):
     """srbd_mpc_step (prep -> fused former + PDIPM -> wrench / torque in ONE kernel, inputs kept
     on chip) against the three-launch sequence it replaces: wrench, torque, solution and the

@@ -137,10 +137,12 @@ def test_mpc_solve_end_to_end():
     assert rel_err_rows(x, ref[0]).max() <= dict(SOLVER_CASES)[K]
 
 
-@pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True)])
+@pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True), (1, True), (3, False),
+                                           (32, True)])
 def test_fused_step_equals_former_plus_solver(N, random_gait):
     """srbd_mpc_solve_fused builds the stage blocks in the solver from the former inputs with the
-    former's own device code, so it reproduces former + solver bit for bit (N = 5 falls back)."""
+    former's own device code, so it reproduces former + solver bit for bit (N = 10, 20: the register
+    kernels; other horizons: the LDS-resident one-launch step kernel, mpc_step_lds.hpp)."""
     B, K = 200, 10
     wl = make_workload(B, N, seed=900 + N, random_gait=random_gait, residuals=random_gait)
     ins = _cuda(wl.inputs)

@@ -9,11 +9,14 @@ RK4 model yields (srbd_constraints.py:83-227) and get_ccs() hands to the solver
 and the oracle's numerical AD Jacobian must have no nonzero outside it.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
 from biped_pympc_amd import layout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _dyn_dependency():
@@ -160,3 +163,20 @@ def test_dense_roundtrip():
     dense = layout.to_dense(v, cp, ri, (14 * N, 24 * N))
     assert np.array_equal(layout.from_dense(dense, cp, ri), v)
     assert np.count_nonzero(dense[0]) == len(ri)
+
+
+def test_sii_entry_order_covers_each_class_once():
+    """The S_ii build's lane -> entry table (csrc/srbd_common.hpp kSiiOrder): the 21 dense x dense
+    entries first, then the 57 with a sparse index, each packed-lower entry exactly once, and the
+    LDS store conflicts it was chosen for (scripts/sii_order.py)."""
+    import re
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from sii_order import dense_cost, sparse_cost
+    src = open(os.path.join(ROOT, "biped_pympc_amd", "csrc", "srbd_common.hpp")).read()
+    body = re.search(r"kSiiOrder\[78\] = \{([^}]*)\}", src).group(1)
+    order = [(int(v) & 15, int(v) >> 4) for v in body.split(",")]
+    assert len(order) == 78 and len(set(order)) == 78 and all(r >= c for r, c in order)
+    sparse = lambda e: (e[0] % 6 >= 3) + (e[1] % 6 >= 3)
+    assert all(sparse(e) == 0 for e in order[:21]) and all(sparse(e) > 0 for e in order[21:])
+    assert dense_cost(order[:21]) <= 5 and sparse_cost(order[21:]) <= 1

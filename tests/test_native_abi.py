@@ -85,10 +85,12 @@ def test_bad_arguments_return_errors_without_touching_the_gpu():
     assert L.srbd_pdipm_cold(10, 5, 0, 1.0, nulls, nulls, None) == 0
     assert L.srbd_pdipm_ccs(10, 5, 4, nulls, nulls, None) != 0
     assert "x_init" in _native.last_error()
-    # the one-launch controller step: N = 10 / 20 only, prep required
+    # the one-launch controller step: any horizon 1..32, prep required
     prep = _native.MPCPrep()
+    assert L.srbd_mpc_step(40, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
+    assert "bad horizon" in _native.last_error()
     assert L.srbd_mpc_step(15, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
-    assert "horizon 10 or 20" in _native.last_error()
+    assert "null foot_wrench" in _native.last_error()
     assert L.srbd_mpc_step(10, 20, 4, 1.0, None, None, None, None, 0, None, None, None, None) != 0
     assert L.srbd_mpc_step(10, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
     assert L.srbd_mpc_step(10, 20, 0, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) == 0
