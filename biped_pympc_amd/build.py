@@ -78,6 +78,7 @@ def build_dropin(kind: str, N: int, K: int | None) -> str:
 HIP_UNITS = {
     "srbd_mpc.hip": ["-DSRBD_SPLIT_REG20"],
     "srbd_reg20.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+    "srbd_regN.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],  # the other register horizons
 }
 
 
@@ -97,15 +98,21 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if force or not _newer(core, srcs):
         # the N = 20 register kernels in their own unit, scheduled with the register-pressure
         # trackers (csrc/reg20.hpp), linked into the same library
-        obj20 = os.path.join(LIB_DIR, "srbd_reg20.o")
-        obj_main = os.path.join(LIB_DIR, "srbd_mpc.o")
-        cmds = [unit_compile_cmd("srbd_reg20.hip", ["-fPIC", "-c", "-o", obj20]),
-                unit_compile_cmd("srbd_mpc.hip", ["-fPIC", "-c", "-o", obj_main]),
-                [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", core, obj_main, obj20]]
-        for cmd in cmds:
+        objs = [os.path.join(LIB_DIR, u.replace(".hip", ".o")) for u in HIP_UNITS]
+        units = [unit_compile_cmd(u, ["-fPIC", "-c", "-o", o]) for u, o in zip(HIP_UNITS, objs)]
+        for cmd in units:
             if verbose:
                 print(" ".join(cmd))
-            _run(cmd)
+        # the units compile in parallel (independent translation units)
+        procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for cmd in units]
+        for cmd, pr in zip(units, procs):
+            out, err = pr.communicate()
+            if pr.returncode != 0:
+                raise RuntimeError(f"build failed: {' '.join(cmd)}\n{out}\n{err}")
+        link = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", core, *objs]
+        if verbose:
+            print(" ".join(link))
+        _run(link)
     for fn, N, K in DROPIN_CONFIGS:
         _build_dropin_lib(fn, N, K, core, force, verbose)
     return core

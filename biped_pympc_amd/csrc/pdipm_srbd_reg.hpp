@@ -34,6 +34,11 @@ namespace srbd {
 // half of every row-parallel phase and gives the SIMD a partner to hide latency behind). The block
 // chains and the per-stage tasks stay on wave 0.
 __host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : 128; }
+// Horizons the register kernels are instantiated for: the equality-row slots need 6 N <= threads
+// per QP, the fused prologue's 17 inputs fit the DV blocks from N = 2, and a two-wave QP splits the
+// stages evenly (even N). N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in
+// srbd_regN.hip; every other horizon runs the LDS-resident kernels.
+__host__ __device__ constexpr bool reg_horizon(int N) { return (N >= 2 && N <= 10) || (N >= 12 && N <= 20 && N % 2 == 0); }
 
 // Ordering of LDS accesses between the threads of one QP. A two-wave QP (N = 20) needs the
 // workgroup barrier. A one-wave QP needs no wait at all: LDS operations of one wavefront are
@@ -62,8 +67,13 @@ struct RegLayout {
                        Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
                        RED = DYm + 2 * N,  // block reductions of a 2-wave QP: 2 slot pairs
-                       total = RED + (TPB > 64 ? 4 : 0);
-  static constexpr int SI = (m + TPB - 1) / TPB, SE = (p + TPB - 1) / TPB, SX = (nx + TPB - 1) / TPB;
+                       end = RED + (TPB > 64 ? 4 : 0),
+                       // the fused prologue's FormerLds scratch from TV on (pads the short horizons)
+                       former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16),
+                       total = end > former ? end : former;
+  // SE: the three equality-row register slots of RegCtx::erow (dynamics rows {0,1,2,6,7,8} and
+  // {3,4,5,9,10,11} of every stage, then the x-moment rows), whatever the horizon
+  static constexpr int SI = (m + TPB - 1) / TPB, SE = 3, SX = (nx + TPB - 1) / TPB;
   static_assert((DV & 1) == 0 && (X & 1) == 0 && (TV & 1) == 0, "16-byte aligned vectors");
 };
 
@@ -325,7 +335,7 @@ struct RegCtx {
   // Equality rows by register slot: slot 0 holds the dynamics rows {0,1,2,6,7,8} of every stage (the
   // dense rows of the u-block N), slot 1 rows {3,4,5,9,10,11} (two force columns each), slot 2 the
   // x-moment rows, so each slot's row formula is the same in every lane.
-  static_assert(SE == 3 && 6 * N <= TPB && 2 * N <= TPB, "equality-row slots");
+  static_assert(6 * N <= TPB && 2 * N <= TPB, "equality-row slots");
   struct ERow {
     int e, i, r;
     bool valid;

@@ -19,6 +19,7 @@
 #include "qp_former.hpp"
 #include "mpc_io.hpp"
 #include "reg20.hpp"
+#include "regN.hpp"
 #include "device_state.hpp"
 
 namespace {
@@ -128,6 +129,14 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   // the stage-invariant kernels solve any other QP of the batch in the same launch (scratch pool)
   if (path != 1)
     if (int rc = attach_scratch(a, s)) return rc;
+  if (path == 0 && srbd::regn::supported(a.N)) {  // the register kernel of another horizon
+    static srbd::LdsAttr cfg_regn[srbd::kMaxN + 1];
+    const size_t lds = srbd::regn::lds_bytes(a.N);
+    if (int rc = ensure_lds_attr(srbd::regn::solver_kernel(a.N), lds, cfg_regn[a.N])) return rc;
+    srbd::regn::launch_solver(a.N, a, lds, s);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_error((int)e, "pdipm_srbd_reg_kernel launch");
+  }
   if (path == 0 && (a.N == 10 || a.N == 20)) {
     if (a.N == 10) {
       if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, cfg_reg10)) return rc;
@@ -336,10 +345,15 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 }
 
 // launch of the fused / controller-step kernel (a fully set up FusedArgs): the register kernels at
-// N = 10 and 20, the LDS-resident one-launch step (mpc_step_lds.hpp) at every other horizon
+// the horizons they are instantiated for (10, 20 and regN.hpp's), the LDS-resident one-launch step
+// (mpc_step_lds.hpp) at every other horizon
 static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
-  static srbd::LdsAttr cfg10, cfg20, cfg_lds;
-  if (a.N != 10 && a.N != 20) {
+  static srbd::LdsAttr cfg10, cfg20, cfg_lds, cfg_regn[srbd::kMaxN + 1];
+  if (srbd::regn::supported(a.N)) {
+    const size_t lds = srbd::regn::lds_bytes(a.N);
+    if (int rc = ensure_lds_attr(srbd::regn::step_kernel(a.N), lds, cfg_regn[a.N])) return rc;
+    srbd::regn::launch_step(a.N, a, lds, st);
+  } else if (a.N != 10 && a.N != 20) {
     const size_t lds = srbd::step_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the one-launch step");
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_lds_kernel<0>, lds, cfg_lds)) return rc;

@@ -1,0 +1,73 @@
+// srbd_regN.hip -- third translation unit of libsrbd_mpc.so: the register-resident solver and
+// fused-step kernels at N = 2..9, 12, 14, 16, 18 (regN.hpp). Launch geometry as in srbd_mpc.hip.
+#define SRBD_NO_GENERAL_KERNEL
+#include "regN.hpp"
+
+#include "pdipm_srbd_reg.hpp"
+
+namespace srbd {
+namespace regn {
+
+#define SRBD_REGN_HORIZONS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(12) X(14) X(16) X(18)
+
+bool supported(int N) {
+  switch (N) {
+#define SRBD_CASE(n) case n: return true;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: return false;
+  }
+}
+
+size_t lds_bytes(int N) {
+  switch (N) {
+#define SRBD_CASE(n) case n: return sizeof(double) * (size_t)RegLayout<n>::total;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: return 0;
+  }
+}
+
+const void* solver_kernel(int N) {
+  switch (N) {
+#define SRBD_CASE(n) case n: return (const void*)pdipm_srbd_reg_kernel<n>;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: return nullptr;
+  }
+}
+
+const void* step_kernel(int N) {
+  switch (N) {
+#define SRBD_CASE(n) case n: return (const void*)mpc_step_reg_kernel<n>;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: return nullptr;
+  }
+}
+
+void launch_solver(int N, const SolverArgs& a, size_t lds, hipStream_t s) {
+  switch (N) {
+#define SRBD_CASE(n) \
+  case n: hipLaunchKernelGGL(pdipm_srbd_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), lds, s, a); break;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: break;
+  }
+}
+
+void launch_step(int N, const FusedArgs& a, size_t lds, hipStream_t s) {
+  switch (N) {
+#define SRBD_CASE(n) \
+  case n: hipLaunchKernelGGL(mpc_step_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), lds, s, a); break;
+    SRBD_REGN_HORIZONS(SRBD_CASE)
+#undef SRBD_CASE
+    default: break;
+  }
+}
+
+static_assert(reg_horizon(2) && reg_horizon(9) && reg_horizon(18) && !reg_horizon(11) && !reg_horizon(1),
+              "SRBD_REGN_HORIZONS lists exactly the register horizons other than 10 and 20");
+
+}  // namespace regn
+}  // namespace srbd

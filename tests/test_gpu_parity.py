@@ -79,15 +79,17 @@ def test_solver_matches_oracle(N, K, tol):
     assert u0_err.max() <= U0_TOL
 
 
-@pytest.mark.parametrize("path", ["auto", "general"])
+@pytest.mark.parametrize("path", ["auto", "lds", "general"])
 @pytest.mark.parametrize("K", [1, 5, 10, 20])
-@pytest.mark.parametrize("N", [1, 2, 3, 5, 32])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 16, 32])
 def test_runtime_horizon_solver_matches_oracle(N, K, path):
-    """Horizons without a compile-time specialisation run the runtime-N LDS-resident kernel
-    (pdipm_srbd_kernel<0>) under the auto path, including the degenerate twisted recursions of
-    N = 1, 2; "general" runs the CCS-table kernel. Per env at the SOLVER_CASES tolerance, or at
-    K = 10 / 20 4x the FP64 floor between the two CPU restatements where that is higher
-    (tests/golden/make_runtime_floor.py: one N = 3 env's z differs by 1e-4 between them at K = 20)."""
+    """Horizons other than 10 and 20 under every solver path: "auto" runs the register kernel at
+    the horizons it is instantiated for (N = 2, 3, 5, 16 here; regN.hpp) and the runtime-N
+    LDS-resident kernel (pdipm_srbd_kernel<0>) at the others (N = 1, 32); "lds" always the latter,
+    including the degenerate twisted recursions of N = 1, 2; "general" the CCS-table kernel. Per env
+    at the SOLVER_CASES tolerance, or 4x the FP64 floor between the two CPU restatements where that
+    is higher (tests/golden/make_runtime_floor.py: one N = 3 env's z differs by 1e-4 between them at
+    K = 20)."""
     from biped_pympc_amd import _native
     B = 48
     wl = make_workload(B, N, seed=500 + N, random_gait=True)
@@ -98,13 +100,11 @@ def test_runtime_horizon_solver_matches_oracle(N, K, path):
     with _native.solver_path(path):
         out = solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K)
         torch.cuda.synchronize()
-    floor = np.load(os.path.join(GOLDEN, "dense_floor_runtime.npz")) if K >= 10 else None
+    floor = np.load(os.path.join(GOLDEN, "dense_floor_runtime.npz"))
     for k, v in enumerate("xszy"):
         o = out[k].cpu().numpy()
         assert np.all(np.isfinite(o))
-        tol = dict(SOLVER_CASES)[K]
-        if floor is not None:
-            tol = np.maximum(tol, 4.0 * floor[f"N{N}_K{K}_{v}"])
+        tol = np.maximum(dict(SOLVER_CASES)[K], 4.0 * floor[f"N{N}_K{K}_{v}"])
         err = rel_err_rows(o, ref[k])
         assert np.all(err <= tol), (N, K, v, err.max())
     assert np.all(np.isfinite(out[5].cpu().numpy()))  # no fallback sentinel left behind
@@ -138,11 +138,11 @@ def test_mpc_solve_end_to_end():
 
 
 @pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True), (1, True), (3, False),
-                                           (32, True)])
+                                           (16, True), (9, False), (32, True), (11, True)])
 def test_fused_step_equals_former_plus_solver(N, random_gait):
     """srbd_mpc_solve_fused builds the stage blocks in the solver from the former inputs with the
-    former's own device code, so it reproduces former + solver bit for bit (N = 10, 20: the register
-    kernels; other horizons: the LDS-resident one-launch step kernel, mpc_step_lds.hpp)."""
+    former's own device code, so it reproduces former + solver bit for bit (the register kernels at
+    N = 3, 5, 9, 10, 16, 20; the LDS-resident one-launch step kernel, mpc_step_lds.hpp, at 1, 11, 32)."""
     B, K = 200, 10
     wl = make_workload(B, N, seed=900 + N, random_gait=random_gait, residuals=random_gait)
     ins = _cuda(wl.inputs)

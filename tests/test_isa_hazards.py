@@ -31,7 +31,7 @@ def _isa(tmp_path, unit):
     return str(out)
 
 
-@pytest.mark.parametrize("unit", ["srbd_mpc.hip", "srbd_reg20.hip"])
+@pytest.mark.parametrize("unit", ["srbd_mpc.hip", "srbd_reg20.hip", "srbd_regN.hip"])
 def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
     from dpp_hazard_check import check
     assert check(_isa(tmp_path, unit)) == 0
