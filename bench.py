@@ -78,10 +78,16 @@ def event_time_ms(fn, reps: int, warm: int = 2) -> float:
     return e0.elapsed_time(e1) / reps
 
 
+def reg_horizon(N: int) -> bool:
+    """Horizons with a register-resident kernel (csrc/pdipm_srbd_reg.hpp reg_horizon)."""
+    return 2 <= N <= 10 or (12 <= N <= 20 and N % 2 == 0)
+
+
 def solver_kernel_name(N: int) -> str:
-    """The kernel that runs the bench step at horizon N: the fused former + solver kernel for N = 10
-    and 20 (srbd_mpc_solve_fused), otherwise the runtime-N solver after qp_former."""
-    return f"mpc_step_reg_kernel<{N}>" if N in (10, 20) else "pdipm_srbd_kernel<0>"
+    """The kernel that runs the bench step at horizon N (srbd_mpc_solve_fused, one launch): the
+    register-resident fused former + solver kernel, or the LDS-resident step kernel at the other
+    horizons."""
+    return f"mpc_step_reg_kernel<{N}>" if reg_horizon(N) else "mpc_step_lds_kernel<0>"
 
 
 def load_pmc(N: int, B: int, K: int):
@@ -211,14 +217,14 @@ def main():
     ms_former = event_time_ms(lambda: solver.qp_former(inputs, N, outputs=qp), a.kernel_reps)
     ms_pdipm = event_time_ms(lambda: solver.pdipm(sol_qp, None, N, K, 1.0, outputs=pd_out),
                              a.kernel_reps)
-    # the step's own kernel: fused former + solver (N = 10, 20), timed on the same inputs
+    # the step's own kernel: fused former + solver (one launch at every horizon), timed on the same inputs
     ms_fused = event_time_ms(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), a.kernel_reps)
-    fused = N in (10, 20)
-    ms_main = ms_fused if fused else ms_pdipm
+    fused = True  # srbd_mpc_solve_fused is one launch at every horizon
+    ms_main = ms_fused
     # the whole controller step: input prep + former + PDIPM + wrench in ONE launch
     # (srbd_mpc_step) vs the same three stages as three launches, on B synthetic robots
     ctrl = None
-    if N in (10, 20) and not a.no_controller:
+    if not a.no_controller:
         from biped_pympc_amd.utils.synthetic import make_controller
         c = make_controller(B, N, seed=77 + rank, device=dev, n_iter=K)
 
