@@ -35,10 +35,10 @@ namespace srbd {
 // chains and the per-stage tasks stay on wave 0.
 __host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : 128; }
 // Horizons the register kernels are instantiated for: the equality-row slots need 6 N <= threads
-// per QP, the fused prologue's 17 inputs fit the DV blocks from N = 2, and a two-wave QP splits the
-// stages evenly (even N). N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in
-// srbd_regN.hip; every other horizon runs the LDS-resident kernels.
-__host__ __device__ constexpr bool reg_horizon(int N) { return (N >= 2 && N <= 10) || (N >= 12 && N <= 20 && N % 2 == 0); }
+// per QP (one wave to N = 10, two to N = 21) and the fused prologue's 17 inputs fit the DV blocks
+// from N = 2. N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in srbd_regN.hip;
+// N = 1 and N > 21 run the LDS-resident kernels.
+__host__ __device__ constexpr bool reg_horizon(int N) { return N >= 2 && N <= 21; }
 
 // Ordering of LDS accesses between the threads of one QP. A two-wave QP (N = 20) needs the
 // workgroup barrier. A one-wave QP needs no wait at all: LDS operations of one wavefront are
@@ -589,7 +589,8 @@ struct RegCtx {
     // are loaded once; only Phi_f^-1 (PHs) changes with the stage.
     // with two waves each takes half of the stages: wave w's lane l < 63 -> class q = 3 w + l / 21
     constexpr int NW = TPB / 64, NQ = 3 * NW;
-    static_assert(N % NW == 0, "stages split evenly over the waves");
+    static_assert(NW <= 2, "one or two waves per QP");
+    constexpr int kHalf = (N + 1) / 2;  // a two-wave QP's sparse pass: wave 0 stages [0, kHalf), wave 1 the rest
     const int lw = lane & 63, wv = lane >> 6;
     if (lw < 63) {  // dense x dense: lw = 21 q' + k -> entry k of stages NQ t + q, q = 3 wv + q'
       const int q = 3 * wv + lw / 21, k = lw - 21 * (lw / 21);
@@ -645,7 +646,7 @@ struct RegCtx {
       for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
       const double k0 = K0[sy], k1 = K1[sy];
 #pragma unroll 2
-      for (int i = wv * (N / NW); i < (wv + 1) * (N / NW); ++i) {  // wave wv's share of the stages
+      for (int i = NW == 1 ? 0 : wv * kHalf; i < (NW == 1 || wv ? N : kHalf); ++i) {  // wave wv's share
         double v = i == 0 ? k0 : k1;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {

@@ -81,11 +81,11 @@ def test_solver_matches_oracle(N, K, tol):
 
 @pytest.mark.parametrize("path", ["auto", "lds", "general"])
 @pytest.mark.parametrize("K", [1, 5, 10, 20])
-@pytest.mark.parametrize("N", [1, 2, 3, 5, 16, 32])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 15, 16, 32])
 def test_runtime_horizon_solver_matches_oracle(N, K, path):
     """Horizons other than 10 and 20 under every solver path: "auto" runs the register kernel at
-    the horizons it is instantiated for (N = 2, 3, 5, 16 here; regN.hpp) and the runtime-N
-    LDS-resident kernel (pdipm_srbd_kernel<0>) at the others (N = 1, 32); "lds" always the latter,
+    the horizons it is instantiated for (2..21: N = 2, 3, 5, 15, 16 here; regN.hpp) and the
+    runtime-N LDS-resident kernel (pdipm_srbd_kernel<0>) at the others (N = 1, 32); "lds" always the latter,
     including the degenerate twisted recursions of N = 1, 2; "general" the CCS-table kernel. Per env
     at the SOLVER_CASES tolerance, or 4x the FP64 floor between the two CPU restatements where that
     is higher (tests/golden/make_runtime_floor.py: one N = 3 env's z differs by 1e-4 between them at
@@ -138,11 +138,13 @@ def test_mpc_solve_end_to_end():
 
 
 @pytest.mark.parametrize("N,random_gait", [(10, False), (10, True), (20, True), (5, True), (1, True), (3, False),
-                                           (16, True), (9, False), (32, True), (11, True)])
+                                           (16, True), (9, False), (32, True), (11, True), (15, True),
+                                           (21, False), (25, True)])
 def test_fused_step_equals_former_plus_solver(N, random_gait):
     """srbd_mpc_solve_fused builds the stage blocks in the solver from the former inputs with the
     former's own device code, so it reproduces former + solver bit for bit (the register kernels at
-    N = 3, 5, 9, 10, 16, 20; the LDS-resident one-launch step kernel, mpc_step_lds.hpp, at 1, 11, 32)."""
+    N = 3, 5, 9, 10, 11, 15, 16, 20, 21; the LDS-resident one-launch step kernel, mpc_step_lds.hpp,
+    at 1, 25, 32)."""
     B, K = 200, 10
     wl = make_workload(B, N, seed=900 + N, random_gait=random_gait, residuals=random_gait)
     ins = _cuda(wl.inputs)
