@@ -80,7 +80,7 @@ def event_time_ms(fn, reps: int, warm: int = 2) -> float:
 
 def reg_horizon(N: int) -> bool:
     """Horizons with a register-resident kernel (csrc/pdipm_srbd_reg.hpp reg_horizon)."""
-    return 2 <= N <= 21
+    return 2 <= N <= 32
 
 
 def solver_kernel_name(N: int) -> str:

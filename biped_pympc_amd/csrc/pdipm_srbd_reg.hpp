@@ -33,12 +33,12 @@ namespace srbd {
 // (the LDS of a longer horizon allows 1 QP per SIMD, so a second wave of the SAME QP takes the other
 // half of every row-parallel phase and gives the SIMD a partner to hide latency behind). The block
 // chains and the per-stage tasks stay on wave 0.
-__host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : 128; }
+__host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : (N <= 21 ? 128 : 192); }
 // Horizons the register kernels are instantiated for: the equality-row slots need 6 N <= threads
-// per QP (one wave to N = 10, two to N = 21) and the fused prologue's 17 inputs fit the DV blocks
-// from N = 2. N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in srbd_regN.hip;
-// N = 1 and N > 21 run the LDS-resident kernels.
-__host__ __device__ constexpr bool reg_horizon(int N) { return N >= 2 && N <= 21; }
+// per QP (one wave to N = 10, two to N = 21, three to N = 32) and the fused prologue's 17 inputs fit
+// the DV blocks from N = 2. N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in
+// srbd_regN.hip; N = 1 runs the LDS-resident kernels.
+__host__ __device__ constexpr bool reg_horizon(int N) { return N >= 2 && N <= 32; }
 
 // Ordering of LDS accesses between the threads of one QP. A two-wave QP (N = 20) needs the
 // workgroup barrier. A one-wave QP needs no wait at all: LDS operations of one wavefront are
@@ -66,8 +66,8 @@ struct RegLayout {
                        X = DV + 80 * N,  // stage blocks of 80 doubles (78 used, kDvSlot)
                        Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
-                       RED = DYm + 2 * N,  // block reductions of a 2-wave QP: 2 slot pairs
-                       end = RED + (TPB > 64 ? 4 : 0),
+                       RED = DYm + 2 * N,  // block reductions of a multi-wave QP: 2 slot sets
+                       end = RED + (TPB > 64 ? 2 * (TPB / 64) : 0),
                        // the fused prologue's FormerLds scratch from TV on (pads the short horizons)
                        former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16),
                        total = end > former ? end : former;
@@ -403,11 +403,14 @@ struct RegCtx {
   __device__ double block_reduce(double v) {
     v = kMin ? wave_min(v) : wave_sum(v);
     if constexpr (TPB > 64) {
-      double* R = at(Lo::RED) + 2 * red_k;
+      constexpr int NW = TPB / 64;
+      double* R = at(Lo::RED) + NW * red_k;
       red_k ^= 1;
       if ((lane & 63) == 0) R[lane >> 6] = v;
       qp_sync<TPB>();
-      v = kMin ? fmin(R[0], R[1]) : R[0] + R[1];
+      v = R[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v = kMin ? fmin(v, R[w]) : v + R[w];
     }
     return v;
   }
@@ -589,8 +592,6 @@ struct RegCtx {
     // are loaded once; only Phi_f^-1 (PHs) changes with the stage.
     // with two waves each takes half of the stages: wave w's lane l < 63 -> class q = 3 w + l / 21
     constexpr int NW = TPB / 64, NQ = 3 * NW;
-    static_assert(NW <= 2, "one or two waves per QP");
-    constexpr int kHalf = (N + 1) / 2;  // a two-wave QP's sparse pass: wave 0 stages [0, kHalf), wave 1 the rest
     const int lw = lane & 63, wv = lane >> 6;
     if (lw < 63) {  // dense x dense: lw = 21 q' + k -> entry k of stages NQ t + q, q = 3 wv + q'
       const int q = 3 * wv + lw / 21, k = lw - 21 * (lw / 21);
@@ -646,7 +647,8 @@ struct RegCtx {
       for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
       const double k0 = K0[sy], k1 = K1[sy];
 #pragma unroll 2
-      for (int i = NW == 1 ? 0 : wv * kHalf; i < (NW == 1 || wv ? N : kHalf); ++i) {  // wave wv's share
+      // wave wv's share of the stages: [wv N / NW, (wv + 1) N / NW) (uneven when NW does not divide N)
+      for (int i = (wv * N) / NW; i < ((wv + 1) * N) / NW; ++i) {
         double v = i == 0 ? k0 : k1;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
@@ -1369,10 +1371,14 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     for (int e = lane; e < nG; e += TPB) bad |= !(Gg[e] == Gg[e % 28]);
     for (int e = lane; e < nz; e += TPB) bad |= !(Hg[e] == Hg[(e < nx ? 0 : nx) + e % 12]);
     bad = __any(bad);
-    if constexpr (TPB > 64) {  // one verdict for the whole QP (both waves leave or both stay)
-      if ((lane & 63) == 0) reinterpret_cast<int*>(smem + Lo::RED)[lane >> 6] = bad;
+    if constexpr (TPB > 64) {  // one verdict for the whole QP (all its waves leave or all stay)
+      int* vr = reinterpret_cast<int*>(smem + Lo::RED);
+      if ((lane & 63) == 0) vr[lane >> 6] = bad;
       qp_sync<TPB>();
-      bad = reinterpret_cast<int*>(smem + Lo::RED)[0] | reinterpret_cast<int*>(smem + Lo::RED)[1];
+      bool any = false;
+#pragma unroll
+      for (int w = 0; w < TPB / 64; ++w) any = any || vr[w];
+      bad = any;
       qp_sync<TPB>();  // RED is reused by the first block reduction
     }
     if (bad) {  // not stage-invariant: the general solve, in this launch (pdipm_general_scratch)

@@ -1,5 +1,5 @@
 // regN.hpp -- the register-resident kernels at the horizons other than 10 and 20 that they support
-// (pdipm_srbd_reg.hpp reg_horizon: 2..21 except 10 and 20), compiled in their own translation unit
+// (pdipm_srbd_reg.hpp reg_horizon: 2..32 except 10 and 20), compiled in their own translation unit
 // (srbd_regN.hip, with the register-pressure trackers as the N = 20 unit) and dispatched by horizon
 // at run time. Every other horizon runs the LDS-resident kernels.
 #pragma once

@@ -1,5 +1,5 @@
 // srbd_regN.hip -- third translation unit of libsrbd_mpc.so: the register-resident solver and
-// fused-step kernels at N = 2..21 except 10 and 20 (regN.hpp). Launch geometry as in srbd_mpc.hip.
+// fused-step kernels at N = 2..32 except 10 and 20 (regN.hpp). Launch geometry as in srbd_mpc.hip.
 #define SRBD_NO_GENERAL_KERNEL
 #include "regN.hpp"
 
@@ -8,8 +8,9 @@
 namespace srbd {
 namespace regn {
 
-#define SRBD_REGN_HORIZONS(X) \
-  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(21)
+#define SRBD_REGN_HORIZONS(X)                                                                     \
+  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(21) \
+  X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
 
 bool supported(int N) {
   switch (N) {
@@ -67,7 +68,7 @@ void launch_step(int N, const FusedArgs& a, size_t lds, hipStream_t s) {
   }
 }
 
-static_assert(reg_horizon(2) && reg_horizon(21) && !reg_horizon(22) && !reg_horizon(1),
+static_assert(reg_horizon(2) && reg_horizon(32) && !reg_horizon(33) && !reg_horizon(1),
               "SRBD_REGN_HORIZONS lists exactly the register horizons other than 10 and 20");
 
 }  // namespace regn

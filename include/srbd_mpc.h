@@ -80,7 +80,7 @@ size_t srbd_mpc_workspace_doubles(int horizon, int batch);
 int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                    double* qp_workspace, double* const* outputs, void* stream);
 
-/* srbd_mpc_solve in ONE kernel at every horizon (the register kernels at N = 10 and 20, the
+/* srbd_mpc_solve in ONE kernel at every horizon (the register kernels at N = 2..32, the
  * LDS-resident step kernel otherwise; a non-auto solver path runs srbd_mpc_solve and needs
  * qp_workspace): the QP is formed in the solver from the former inputs and never written, except
  * f, b, d into their qp_workspace slots when qp_workspace != NULL (NULL: no QP data leaves the
@@ -93,7 +93,7 @@ int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const do
 size_t srbd_solver_lds_bytes(int horizon);
 
 /* Solver kernel selection: 0 = auto (default): a stage-invariant kernel for stage-invariant QPs
- * (every QP qp_former emits; register-resident at N = 10 and 20, LDS-resident otherwise), the general
+ * (every QP qp_former emits; register-resident at N = 2..32, LDS-resident otherwise), the general
  * kernel for any other QP in the batch; 1 = general kernel only; 2 = LDS-resident stage-invariant
  * kernel at every horizon (plus the general fallback).
  * Results agree to round-off (tests/test_gpu_parity.py). Per device: applies to calls made while

@@ -1,7 +1,7 @@
 """Generate tests/golden/dense_floor_runtime.npz (committed fixture; CPU, ~1 min on 8 cores).
 
 For the runtime-horizon workloads of tests/test_gpu_parity.py::test_runtime_horizon_solver_matches_oracle
-(N in {1, 2, 3, 5, 15, 16, 32}, B = 48, randomized gait, seed 500 + N, GPU-caller init) at K = 1, 5, 10, 20:
+(N in {1, 2, 3, 5, 15, 16, 25, 32}, B = 48, randomized gait, seed 500 + N, GPU-caller init) at K = 1, 5, 10, 20:
 the per-env relative error of x, s, z, y between the two independent CPU restatements of the
 solver -- the C oracle (sparse LDL^T) and oracle/pdipm_dense.py (dense LU of the full KKT). That
 spread is the FP64 floor of the comparison; the GPU test allows max(tol, 4 x floor) per env.
@@ -21,7 +21,7 @@ from oracle import oracle  # noqa: E402
 from oracle.pdipm_dense import pdipm_dense  # noqa: E402
 from tests._util import rel_err_rows  # noqa: E402
 
-HORIZONS = (1, 2, 3, 5, 15, 16, 32)
+HORIZONS = (1, 2, 3, 5, 15, 16, 25, 32)
 B = 48
 
 

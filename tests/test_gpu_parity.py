@@ -81,11 +81,11 @@ def test_solver_matches_oracle(N, K, tol):
 
 @pytest.mark.parametrize("path", ["auto", "lds", "general"])
 @pytest.mark.parametrize("K", [1, 5, 10, 20])
-@pytest.mark.parametrize("N", [1, 2, 3, 5, 15, 16, 32])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 15, 16, 25, 32])
 def test_runtime_horizon_solver_matches_oracle(N, K, path):
     """Horizons other than 10 and 20 under every solver path: "auto" runs the register kernel at
-    the horizons it is instantiated for (2..21: N = 2, 3, 5, 15, 16 here; regN.hpp) and the
-    runtime-N LDS-resident kernel (pdipm_srbd_kernel<0>) at the others (N = 1, 32); "lds" always the latter,
+    the horizons it is instantiated for (2..32: N = 2, 3, 5 one wave per QP, 15, 16 two, 25, 32 three;
+    regN.hpp) and the runtime-N LDS-resident kernel (pdipm_srbd_kernel<0>) at N = 1; "lds" always the latter,
     including the degenerate twisted recursions of N = 1, 2; "general" the CCS-table kernel. Per env
     at the SOLVER_CASES tolerance, or 4x the FP64 floor between the two CPU restatements where that
     is higher (tests/golden/make_runtime_floor.py: one N = 3 env's z differs by 1e-4 between them at
