@@ -1,6 +1,6 @@
 """Static instruction mix per solver phase of the fused N=10 kernel (diagnostic, CPU only).
 
-python scripts/isa_phase_mix.py [extra hipcc flags...]
+python scripts/isa_phase_mix.py [--top K] [extra hipcc flags...]
 
 Builds the fused kernel with scripts/phase_prof.hpp force-included (s_memtime stamps at the phase boundaries, see
 srbd_common.hpp), splits the kernel's ISA at the stamps and counts instruction classes per
@@ -28,6 +28,10 @@ CLASSES = [
 
 
 def main():
+    top = 0
+    if len(sys.argv) > 2 and sys.argv[1] == "--top":
+        top = int(sys.argv[2])
+        del sys.argv[1:3]
     out = "/tmp/isa_phase_mix.s"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
                     "--cuda-device-only", "-S", "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), *sys.argv[1:], "-o", out,
@@ -61,6 +65,12 @@ def main():
             else:
                 other += 1
         print(f"{k:>4} {len(seg):>6} " + " ".join(f"{cnt[c]:>7}" for c, _ in CLASSES) + f"  {other}")
+        if top:  # the segment's most frequent non-FP64 vector instructions
+            hist = {}
+            for op in seg:
+                if op.startswith("v_") and not re.match(CLASSES[0][1] + "|" + CLASSES[1][1], op):
+                    hist[op] = hist.get(op, 0) + 1
+            print("       " + ", ".join(f"{o} {n}" for o, n in sorted(hist.items(), key=lambda x: -x[1])[:top]))
 
 
 if __name__ == "__main__":
