@@ -57,10 +57,18 @@ __device__ __forceinline__ void qp_sync() {
   }
 }
 
+// LDS bank spreading of the stage-invariant blocks (a ds_read_b64 serves 32 lanes per pass from 64
+// 4-byte banks): the u-block N is stored with row stride kNdS = 13, so the lanes of a row-parallel
+// pass reading rows {0,1,2,6,7,8} (or all 12 rows, S_ii) of one column hit 12 distinct bank pairs
+// (stride 12: rows r and r + 8 share a bank); G's foot-1 rows start kGfPad = 4 doubles after foot 0's
+// (g_row), so the 8 lanes of a stage reading one row of both feet in G^T z use 16 distinct banks.
+constexpr int kNdS = 13, kGfPad = 4, kGfSize = 64 + kGfPad;
+__host__ __device__ constexpr int nd_idx(int r, int c) { return r * kNdS + c; }
+
 template <int N, int TPB = reg_tpb(N)>
 struct RegLayout {
   static constexpr int nz = 24 * N, m = 16 * N, p = 14 * N, nx = 12 * N;
-  static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 144, K0 = Gf + 66, K1 = K0 + 78,
+  static constexpr int Mc = 0, Cc = Mc + 24, Nd = Cc + 48, Gf = Nd + 12 * kNdS, K0 = Gf + kGfSize, K1 = K0 + 78,
                        Pd = K1 + 78, IX = Pd + 12, Hu = IX + 12, SG = Hu + 24, TRI = SG + 16,
                        DV = TRI + 10,
                        X = DV + 80 * N,  // stage blocks of 80 doubles (78 used, kDvSlot)
@@ -299,12 +307,12 @@ __device__ __forceinline__ double drow12(const double* row, const double* v) {
 // stored zeros make the formula exact for every col); kForce = false skips them (col >= 6 known)
 template <bool kForce = true>
 __device__ __forceinline__ double ncol(const double* nd, int col, const double* v, int p) {
-  double a0 = nd[col] * v[0] + nd[12 + col] * v[1];
-  double a1 = nd[24 + col] * v[2] + nd[72 + col] * v[6];
-  double a2 = nd[84 + col] * v[7] + nd[96 + col] * v[8];
+  double a0 = nd[nd_idx(0, col)] * v[0] + nd[nd_idx(1, col)] * v[1];
+  double a1 = nd[nd_idx(2, col)] * v[2] + nd[nd_idx(6, col)] * v[6];
+  double a2 = nd[nd_idx(7, col)] * v[7] + nd[nd_idx(8, col)] * v[8];
   if (kForce) {
-    a0 += nd[12 * (3 + p) + col] * v[3 + p];
-    a1 += nd[12 * (9 + p) + col] * v[9 + p];
+    a0 += nd[nd_idx(3 + p, col)] * v[3 + p];
+    a1 += nd[nd_idx(9 + p, col)] * v[9 + p];
   }
   return (a0 + a1) + a2;
 }
@@ -315,9 +323,8 @@ __device__ __forceinline__ double ncol(const double* nd, int col, const double* 
 // stored structural zero, so the formula stays uniform across lanes).
 __host__ __device__ constexpr int g_other(int k) { return k < 2 ? 0 : (k < 4 ? 1 : (k < 6 ? 3 : 0)); }
 
-// G rows in LDS: row k (= 8 f + k', foot f) at 4 k + f, i.e. foot 1's rows one double further:
-// lanes reading the same column of both feet (or of rows k and k + 8) then hit different banks
-__host__ __device__ constexpr int g_row(int k) { return 4 * k + (k >> 3); }
+// G rows in LDS: row k (= 8 f + k', foot f) at 4 k + kGfPad f (see kGfPad)
+__host__ __device__ constexpr int g_row(int k) { return 4 * k + kGfPad * (k >> 3); }
 
 // (G xu)_k over row k's structural nonzeros (fz and the other column)
 __device__ __forceinline__ double grow4(const double* gf, int k, const double* xu) {
@@ -360,10 +367,10 @@ struct RegCtx {
   template <int t>
   __device__ static double nrow(const double* nd, int r, const double* u) {
     if constexpr (t == 0) {
-      return drow12(nd + 12 * r, u);
+      return drow12(nd + nd_idx(r, 0), u);
     } else {
       const int p = r % 3;
-      return nd[12 * r + p] * u[p] + nd[12 * r + 3 + p] * u[3 + p];
+      return nd[nd_idx(r, p)] * u[p] + nd[nd_idx(r, 3 + p)] * u[3 + p];
     }
   }
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
@@ -604,8 +611,8 @@ struct RegCtx {
         double vr[4], vc[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          vr[a] = Nd[r * 12 + foot_colj(f, a)];
-          vc[a] = Nd[c * 12 + foot_colj(f, a)];
+          vr[a] = Nd[nd_idx(r, foot_colj(f, a))];
+          vc[a] = Nd[nd_idx(c, foot_colj(f, a))];
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -639,9 +646,9 @@ struct RegCtx {
       int po[4];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        const double ns = Nd[sp * 12 + foot_colj(f, as)];
+        const double ns = Nd[nd_idx(sp, foot_colj(f, as))];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) wn[f][b] = ns * Nd[dn * 12 + foot_colj(f, b)];
+        for (int b = 0; b < 4; ++b) wn[f][b] = ns * Nd[nd_idx(dn, foot_colj(f, b))];
       }
 #pragma unroll
       for (int b = 0; b < 4; ++b) po[b] = sym_idx(as, b);
@@ -1277,9 +1284,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       const int r = e / 12, j = e % 12;
       const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
       Md[e] = (N >= 2 && om >= 0) ? F.XB[om] : 0.0;
-      Nd[e] = on >= 0 ? F.UB[on] : 0.0;
+      Nd[nd_idx(r, j)] = on >= 0 ? F.UB[on] : 0.0;
     }
-    for (int e = lane; e < 66; e += TPB) Gf[e] = 0.0;  // 16 rows x 4 (+ the foot-1 pad)
+    for (int e = lane; e < kGfSize; e += TPB) Gf[e] = 0.0;  // 16 rows x 4 (+ the foot-1 pad)
     if (lane < 12) {
       Pd[lane] = F.XB[c_tab.cpx[lane]];
       Hu[lane] = P[14][lane];       // H = diag(Q.., R..): u part R
@@ -1343,9 +1350,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       const int r = e / 12, j = e % 12;
       const int om = c_tab.Mi[r][j], on = c_tab.Ni[r][j];
       Md[e] = (N >= 2 && om >= 0) ? Ag[a_xblock(1) + om] : 0.0;
-      Nd[e] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
+      Nd[nd_idx(r, j)] = on >= 0 ? Ag[a_ublock(N, 0) + on] : 0.0;
     }
-    for (int e = lane; e < 66; e += TPB) Gf[e] = 0.0;  // 16 rows x 4 (+ the foot-1 pad)
+    for (int e = lane; e < kGfSize; e += TPB) Gf[e] = 0.0;  // 16 rows x 4 (+ the foot-1 pad)
     if (lane < 12) {
       Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
       Hu[lane] = Hg[nx + lane];
@@ -1423,8 +1430,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     int r, c;
     tri_rc(e, r, c);
     double k0 = (r == c) ? Pd[r] * Pd[r] * IX[r] + kDelta : 0.0;
-    k0 += Nd[r * 12 + 6] * Nd[c * 12 + 6] * SG[0] + Nd[r * 12 + 8] * Nd[c * 12 + 8] * SG[1] +
-          Nd[r * 12 + 9] * Nd[c * 12 + 9] * SG[2] + Nd[r * 12 + 11] * Nd[c * 12 + 11] * SG[3];
+    k0 += Nd[nd_idx(r, 6)] * Nd[nd_idx(c, 6)] * SG[0] + Nd[nd_idx(r, 8)] * Nd[nd_idx(c, 8)] * SG[1] +
+          Nd[nd_idx(r, 9)] * Nd[nd_idx(c, 9)] * SG[2] + Nd[nd_idx(r, 11)] * Nd[nd_idx(c, 11)] * SG[3];
     double k1 = k0;
 #pragma unroll
     for (int j = 0; j < 12; ++j) k1 += Md[r * 12 + j] * Md[c * 12 + j] * IX[j];

@@ -42,7 +42,7 @@ SII_MFMA = r'''    // S_ii = K + P Phi_u,i^-1 P^T on the matrix cores (v_mfma_f6
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int kk = 4 * s + kq;
-        pa[s] = r16 < 12 ? Nd[r16 * 12 + foot_colj(kk >> 2, kk & 3)] : 0.0;
+        pa[s] = r16 < 12 ? Nd[nd_idx(r16, foot_colj(kk >> 2, kk & 3))] : 0.0;
       }
       // this lane's four S entries (row kq + 4 j, column r16): packed-slot offset and K index;
       // only the lower triangle is stored (the packed block keeps one copy of each pair)
