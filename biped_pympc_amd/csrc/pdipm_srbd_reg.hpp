@@ -1210,7 +1210,10 @@ template <int N, bool kFused>
 __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const FusedArgs& fa) {
   using Lo = RegLayout<N>;
   constexpr int TPB = reg_tpb(N);
-  extern __shared__ __attribute__((aligned(16))) double smem[];
+  // Static LDS sized by the horizon's layout (launched with 0 dynamic bytes): the addresses are
+  // compile-time constants that fold into the instructions (a dynamic-LDS base is a link-time symbol
+  // the backend re-adds as a literal 0 in every address computation: 118 v_add_u32 per kernel at N = 10)
+  __shared__ __attribute__((aligned(16))) double smem[Lo::total];
   const int env = xcd_item(blockIdx.x, gridDim.x);
   if (env >= (kFused ? fa.batch : args.batch)) return;
   const int lane = threadIdx.x;
@@ -1654,14 +1657,27 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   }
 }
 
-// 2 waves per SIMD: 2 one-wave QPs (N <= 10) or 1 two-wave QP (N = 20) per SIMD, <= 256 registers
+// Device code generation of the register kernels: no SILoadStoreOptimizer (the backend pass that
+// pairs adjacent ds_read_b64 / ds_write_b64 into ds_read2_b64 / ds_write2_b64). A read2_b64 takes
+// 8 LDS cycles (two accesses of 4 x 16 lanes, 32-bank mapping) where two ds_read_b64 take 4, and
+// LDS is this kernel's busiest unit: without the pairing the fused N = 10 step runs 2.9 % faster
+// (0.666 -> 0.646 ms; 12,955 -> 14,644 LDS instructions, 190k -> 184k wave cycles per QP;
+// profiles/r03/no_ds_pairing.txt). Pairs the IR load-store vectorizer forms are kept.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SRBD_NO_DS_PAIRING __attribute__((target("no-load-store-opt")))
+#else
+#define SRBD_NO_DS_PAIRING
+#endif
+
+// at most 2 waves per SIMD (<= 256 registers): 2 one-wave QPs (N <= 10) per SIMD, or the waves of
+// two-wave (N <= 21) and three-wave (N <= 32) QPs
 template <int N>
-__global__ __launch_bounds__(reg_tpb(N), 2) void pdipm_srbd_reg_kernel(SolverArgs args) {
+__global__ __launch_bounds__(reg_tpb(N), 2) SRBD_NO_DS_PAIRING void pdipm_srbd_reg_kernel(SolverArgs args) {
   reg_kernel_body<N, false>(args, FusedArgs{});
 }
 
 template <int N>
-__global__ __launch_bounds__(reg_tpb(N), 2) void mpc_step_reg_kernel(FusedArgs fa) {
+__global__ __launch_bounds__(reg_tpb(N), 2) SRBD_NO_DS_PAIRING void mpc_step_reg_kernel(FusedArgs fa) {
   reg_kernel_body<N, true>(SolverArgs{}, fa);
 }
 

@@ -13,7 +13,7 @@ struct FusedArgs;
 namespace reg20 {
 const void* solver_kernel();  // pdipm_srbd_reg_kernel<20>
 const void* step_kernel();    // mpc_step_reg_kernel<20>
-void launch_solver(const SolverArgs& a, size_t lds, hipStream_t s);
-void launch_step(const FusedArgs& a, size_t lds, hipStream_t s);
+void launch_solver(const SolverArgs& a, hipStream_t s);
+void launch_step(const FusedArgs& a, hipStream_t s);
 }  // namespace reg20
 }  // namespace srbd

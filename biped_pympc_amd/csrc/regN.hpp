@@ -14,7 +14,8 @@ bool supported(int N);        // a register kernel instantiated here for this ho
 size_t lds_bytes(int N);      // RegLayout<N> in bytes
 const void* solver_kernel(int N);
 const void* step_kernel(int N);
-void launch_solver(int N, const SolverArgs& a, size_t lds, hipStream_t s);
-void launch_step(int N, const FusedArgs& a, size_t lds, hipStream_t s);
+// static LDS (RegLayout<N>): launched with 0 dynamic bytes
+void launch_solver(int N, const SolverArgs& a, hipStream_t s);
+void launch_step(int N, const FusedArgs& a, hipStream_t s);
 }  // namespace regn
 }  // namespace srbd

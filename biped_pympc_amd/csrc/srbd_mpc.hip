@@ -44,7 +44,9 @@ size_t solver_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::SolverLay
 size_t fast_lds_bytes(int N) { return sizeof(double) * (size_t)srbd::FastLayout(N).total; }
 constexpr size_t kRegLds10 = sizeof(double) * (size_t)srbd::RegLayout<10>::total;
 constexpr size_t kRegLds20 = sizeof(double) * (size_t)srbd::RegLayout<20>::total;
+// the register kernels' LDS is static (RegLayout<N>::total doubles per workgroup)
 static_assert(kRegLds10 <= 20 * 1024, "N=10 register kernel must fit 8 QPs per CU");
+static_assert(kRegLds20 <= 40 * 1024, "N=20 register kernel must fit 4 QPs per CU");
 
 // The HIP device current at this call (-1 if none / out of range for the per-device state)
 int current_device() {
@@ -123,31 +125,25 @@ int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
 
 int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
-  static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20, cfg_reg10, cfg_reg20;
+  static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20;
   srbd::SolverArgs a = a0;
   const int path = solver_path();
   // the stage-invariant kernels solve any other QP of the batch in the same launch (scratch pool)
   if (path != 1)
     if (int rc = attach_scratch(a, s)) return rc;
   if (path == 0 && srbd::regn::supported(a.N)) {  // the register kernel of another horizon
-    static srbd::LdsAttr cfg_regn[srbd::kMaxN + 1];
-    const size_t lds = srbd::regn::lds_bytes(a.N);
-    if (int rc = ensure_lds_attr(srbd::regn::solver_kernel(a.N), lds, cfg_regn[a.N])) return rc;
-    srbd::regn::launch_solver(a.N, a, lds, s);
+    srbd::regn::launch_solver(a.N, a, s);  // static LDS (RegLayout)
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_error((int)e, "pdipm_srbd_reg_kernel launch");
   }
   if (path == 0 && (a.N == 10 || a.N == 20)) {
     if (a.N == 10) {
-      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<10>, kRegLds10, cfg_reg10)) return rc;
-      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, s, a);
+      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<10>, dim3(a.batch), dim3(64), 0, s, a);
     } else {
 #ifdef SRBD_SPLIT_REG20
-      if (int rc = ensure_lds_attr(srbd::reg20::solver_kernel(), kRegLds20, cfg_reg20)) return rc;
-      srbd::reg20::launch_solver(a, kRegLds20, s);
+      srbd::reg20::launch_solver(a, s);
 #else
-      if (int rc = ensure_lds_attr((const void*)srbd::pdipm_srbd_reg_kernel<20>, kRegLds20, cfg_reg20)) return rc;
-      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, s, a);
+      hipLaunchKernelGGL(srbd::pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), 0, s, a);
 #endif
     }
     hipError_t e = hipGetLastError();
@@ -348,26 +344,21 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 // the horizons they are instantiated for (10, 20 and regN.hpp's), the LDS-resident one-launch step
 // (mpc_step_lds.hpp) at every other horizon
 static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
-  static srbd::LdsAttr cfg10, cfg20, cfg_lds, cfg_regn[srbd::kMaxN + 1];
+  static srbd::LdsAttr cfg_lds;
   if (srbd::regn::supported(a.N)) {
-    const size_t lds = srbd::regn::lds_bytes(a.N);
-    if (int rc = ensure_lds_attr(srbd::regn::step_kernel(a.N), lds, cfg_regn[a.N])) return rc;
-    srbd::regn::launch_step(a.N, a, lds, st);
+    srbd::regn::launch_step(a.N, a, st);  // static LDS (RegLayout)
   } else if (a.N != 10 && a.N != 20) {
     const size_t lds = srbd::step_lds_bytes(a.N);
     if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the one-launch step");
     if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_lds_kernel<0>, lds, cfg_lds)) return rc;
     hipLaunchKernelGGL(srbd::mpc_step_lds_kernel<0>, dim3(a.batch), dim3(64), lds, st, a);
   } else if (a.N == 10) {
-    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<10>, kRegLds10, cfg10)) return rc;
-    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(a.batch), dim3(64), kRegLds10, st, a);
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<10>, dim3(a.batch), dim3(64), 0, st, a);
   } else {
 #ifdef SRBD_SPLIT_REG20
-    if (int rc = ensure_lds_attr(srbd::reg20::step_kernel(), kRegLds20, cfg20)) return rc;
-    srbd::reg20::launch_step(a, kRegLds20, st);
+    srbd::reg20::launch_step(a, st);
 #else
-    if (int rc = ensure_lds_attr((const void*)srbd::mpc_step_reg_kernel<20>, kRegLds20, cfg20)) return rc;
-    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), kRegLds20, st, a);
+    hipLaunchKernelGGL(srbd::mpc_step_reg_kernel<20>, dim3(a.batch), dim3(srbd::reg_tpb(20)), 0, st, a);
 #endif
   }
   hipError_t e = hipGetLastError();

@@ -9,11 +9,11 @@ namespace srbd {
 namespace reg20 {
 const void* solver_kernel() { return (const void*)pdipm_srbd_reg_kernel<20>; }
 const void* step_kernel() { return (const void*)mpc_step_reg_kernel<20>; }
-void launch_solver(const SolverArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(reg_tpb(20)), lds, s, a);
+void launch_solver(const SolverArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(pdipm_srbd_reg_kernel<20>, dim3(a.batch), dim3(reg_tpb(20)), 0, s, a);
 }
-void launch_step(const FusedArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(mpc_step_reg_kernel<20>, dim3(a.batch), dim3(reg_tpb(20)), lds, s, a);
+void launch_step(const FusedArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(mpc_step_reg_kernel<20>, dim3(a.batch), dim3(reg_tpb(20)), 0, s, a);
 }
 }  // namespace reg20
 }  // namespace srbd

@@ -48,20 +48,20 @@ const void* step_kernel(int N) {
   }
 }
 
-void launch_solver(int N, const SolverArgs& a, size_t lds, hipStream_t s) {
+void launch_solver(int N, const SolverArgs& a, hipStream_t s) {
   switch (N) {
 #define SRBD_CASE(n) \
-  case n: hipLaunchKernelGGL(pdipm_srbd_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), lds, s, a); break;
+  case n: hipLaunchKernelGGL(pdipm_srbd_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), 0, s, a); break;
     SRBD_REGN_HORIZONS(SRBD_CASE)
 #undef SRBD_CASE
     default: break;
   }
 }
 
-void launch_step(int N, const FusedArgs& a, size_t lds, hipStream_t s) {
+void launch_step(int N, const FusedArgs& a, hipStream_t s) {
   switch (N) {
 #define SRBD_CASE(n) \
-  case n: hipLaunchKernelGGL(mpc_step_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), lds, s, a); break;
+  case n: hipLaunchKernelGGL(mpc_step_reg_kernel<n>, dim3(a.batch), dim3(reg_tpb(n)), 0, s, a); break;
     SRBD_REGN_HORIZONS(SRBD_CASE)
 #undef SRBD_CASE
     default: break;
