@@ -8,9 +8,31 @@
 namespace srbd {
 namespace regn {
 
-#define SRBD_REGN_HORIZONS(X)                                                                     \
-  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(21) \
-  X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+// The horizons in six parts of about equal compile time; SRBD_REGN_PART = k (0..5) instantiates
+// part k only -- for the ISA audit (tests/test_isa_hazards.py), which compiles the parts in parallel.
+// The product build defines no part: every horizon.
+#define SRBD_REGN_P0(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(11) X(12) X(13)
+#define SRBD_REGN_P1(X) X(14) X(15) X(16) X(17) X(18)
+#define SRBD_REGN_P2(X) X(19) X(21) X(22) X(23)
+#define SRBD_REGN_P3(X) X(24) X(25) X(26)
+#define SRBD_REGN_P4(X) X(27) X(28) X(29)
+#define SRBD_REGN_P5(X) X(30) X(31) X(32)
+#if !defined(SRBD_REGN_PART)
+#define SRBD_REGN_HORIZONS(X) \
+  SRBD_REGN_P0(X) SRBD_REGN_P1(X) SRBD_REGN_P2(X) SRBD_REGN_P3(X) SRBD_REGN_P4(X) SRBD_REGN_P5(X)
+#elif SRBD_REGN_PART == 0
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P0(X)
+#elif SRBD_REGN_PART == 1
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P1(X)
+#elif SRBD_REGN_PART == 2
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P2(X)
+#elif SRBD_REGN_PART == 3
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P3(X)
+#elif SRBD_REGN_PART == 4
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P4(X)
+#else
+#define SRBD_REGN_HORIZONS(X) SRBD_REGN_P5(X)
+#endif
 
 bool supported(int N) {
   switch (N) {

@@ -20,21 +20,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
+REGN_PARTS = 6  # csrc/srbd_regN.hip SRBD_REGN_PART: its horizons in six parts, compiled in parallel
+
+
 def _isa(tmp_path, unit):
+    """Device ISA of one translation unit: a list of .s files (srbd_regN.hip: one per horizon part,
+    the parts compiled concurrently with the product flags plus -DSRBD_REGN_PART=k)."""
     from biped_pympc_amd.build import HIPCC, unit_compile_cmd
     if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
         pytest.skip("hipcc not available")
-    out = tmp_path / (unit + ".s")
-    cmd = unit_compile_cmd(unit, ["--cuda-device-only", "-S", "-o", str(out)])
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr[-2000:]
-    return str(out)
+    parts = [[f"-DSRBD_REGN_PART={k}"] for k in range(REGN_PARTS)] if unit == "srbd_regN.hip" else [[]]
+    outs, procs = [], []
+    for k, defs in enumerate(parts):
+        out = tmp_path / f"{unit}.{k}.s"
+        cmd = unit_compile_cmd(unit, [*defs, "--cuda-device-only", "-S", "-o", str(out)])
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True))
+        outs.append(str(out))
+    for p in procs:
+        err = p.communicate()[1]
+        assert p.returncode == 0, err[-2000:]
+    return outs
 
 
 @pytest.mark.parametrize("unit", ["srbd_mpc.hip", "srbd_reg20.hip", "srbd_regN.hip"])
 def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
     from dpp_hazard_check import check
-    assert check(_isa(tmp_path, unit)) == 0
+    for s in _isa(tmp_path, unit):
+        assert check(s) == 0, s
 
 
 def test_checker_detects_planted_hazards(tmp_path):
