@@ -436,6 +436,10 @@ struct RegCtx {
     asm volatile("" : "+v"(l));
     return l;
   }
+  // Slot t of a row-parallel pass over n rows (row = lane + TPB t) lies wholly inside [0, n): its row
+  // guard is then constant-true and compiles to nothing -- the opaque lane of fresh_lane() hides
+  // lane < TPB from the compiler, which otherwise branches on every slot's guard
+  __device__ static constexpr bool full_slot(int t, int n) { return TPB * (t + 1) <= n; }
 
   // --------------------------------------------------------------------- residuals ----
   template <int t>
@@ -470,7 +474,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
       const int c = lane + TPB * t;
-      if (c < nx) {
+      if (full_slot(t, nx) || c < nx) {
         const int k = c / 12 + 1, j = c % 12;
         const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
@@ -481,7 +485,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // r_x, u columns: H_u u + f + G^T z + N^T y + e-rows (LDS)
       const int c = lane + TPB * t;
-      if (c < nx) {
+      if (full_slot(t, nx) || c < nx) {
         const int i = c / 12, j = c % 12;
         const double v = Hu[j] * X[nx + c] + fu[t];
         double gz = 0.0;
@@ -518,7 +522,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {  // r_s = G u + s - h (owner regs)
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q / 16, k = q % 16;
         const double v = grow4(Gf, k, X + nx + 12 * i);
         rs[t] = (v + s[t]) - hv[t];
@@ -556,7 +560,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         wd[t] = rcp3(s[t]) * z[t] + kDelta;  // correctly rounded reciprocals (rcp3), not IEEE division
         di[t] = rcp3(1.0 + kDelta * wd[t]);
         VV[q] = di[t] * wd[t];  // Lambda, shared with the foot tasks
@@ -836,7 +840,7 @@ struct RegCtx {
       for (int t = 0; t < SI; ++t) {
         const int q = lane + TPB * t;
         e3r[t] = 0.0;
-        if (q < m) {
+        if (RegCtx<N>::full_slot(t, m) || q < m) {
           const int i = q / 16, k = q % 16;
           const double gd = grow4(Gf, k, TV + nx + 12 * i);
           const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
@@ -889,7 +893,7 @@ struct RegCtx {
     if (kAff) {  // Z is dead from here on: it keeps e3 for solve_finish<true, true>
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (lane + TPB * t < m) Zd[lane + TPB * t] = e3r[t];
+        if (full_slot(t, m) || lane + TPB * t < m) Zd[lane + TPB * t] = e3r[t];
     }
     rho_slot<0, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
     rho_slot<1, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
@@ -908,7 +912,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const double si = rcp3(s[t]);
         double r2 = -(si * (s[t] * z[t]));
         if (kMode == 1) r2 = r2 + -(si * (s[t] * z[t] + ds[t] * dz[t] - smu));
@@ -922,7 +926,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
       const int c = lane + TPB * t;
-      if ((kMode == 0 || rx) && c < nx) TV[c] = -rxx[t] * IX[c % 12];
+      if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[c % 12];
     }
     qp_sync<TPB>();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
@@ -1069,7 +1073,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int c = lane + TPB * t;
-      if (!kAffine && c < nx) {
+      if (!kAffine && (full_slot(t, nx) || c < nx)) {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         if (k < N) aty += mcol(Mc, j, QV + 12 * k);
@@ -1117,7 +1121,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {  // dz, ds (owner regs)
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q / 16, k = q % 16;
         const double gd = grow4(Gf, k, TV + nx + 12 * i);
         const double vq = VV[q];
@@ -1145,7 +1149,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const bool c = dv[t] < 0.0;
         const double a = -v[t] * rcp3(dv[t]);
         mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
@@ -1160,7 +1164,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const bool c = dv[t] < 0.0;
         const double a = -v[t] * rcp3(dv[t]);
         mn = fmin(mn, (c ? a : 0.0) + (!c ? 1.0 : 0.0));
@@ -1453,7 +1457,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         C.s[t] = fmax(C.hvr[t] - ccs_gx(solver_in(args, 1) + (size_t)env * 28 * N, q, X + nx), 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
@@ -1469,7 +1473,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         C.s[t] = sg[q];
         C.z[t] = zg[q];
         Z[q] = C.z[t];
@@ -1481,7 +1485,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         C.s[t] = fmax(C.hvr[t] - 0.0, 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
@@ -1522,7 +1526,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       bool p = false;
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (l + TPB * t < m) p = p || (C.s[t] <= 1e-8);
+        if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m) p = p || (C.s[t] <= 1e-8);
       degen = C.block_any(p);
     }
     int ul = C.fresh_lane();
@@ -1530,10 +1534,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
       for (int t = 0; t < Lo::SX; ++t)
-        if (ul + TPB * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + TPB * t] * RXu[ul + TPB * t];
+        if (RegCtx<N>::full_slot(t, nx) || ul + TPB * t < nx) a += C.rxx[t] * C.rxx[t] + RXu[ul + TPB * t] * RXu[ul + TPB * t];
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (ul + TPB * t < m) b += C.rs[t] * C.rs[t];
+        if (RegCtx<N>::full_slot(t, m) || ul + TPB * t < m) b += C.rs[t] * C.rs[t];
 #pragma unroll
       for (int t = 0; t < Lo::SE; ++t)
         if (RegCtx<N>::erow(ul, t).valid) c += C.re[t] * C.re[t];
@@ -1560,7 +1564,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     ul = C.fresh_lane();
 #pragma unroll
     for (int t = 0; t < SI; ++t)
-      if (ul + TPB * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
+      if (RegCtx<N>::full_slot(t, m) || ul + TPB * t < m) sza += (C.s[t] + ap * C.ds[t]) * (C.z[t] + ad * C.dz[t]);
     const double mu_aff = C.block_sum(sza) / m;
     const double ratio = mu_aff / mu;
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
@@ -1578,11 +1582,15 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     qp_sync<TPB>();
     double szn = 0.0;
     ul = C.fresh_lane();
-    for (int e = ul; e < nz; e += TPB) X[e] = X[e] + apc * TV[e];
+#pragma unroll
+    for (int t = 0; t < (nz + TPB - 1) / TPB; ++t) {
+      const int e = ul + TPB * t;
+      if (RegCtx<N>::full_slot(t, nz) || e < nz) X[e] = X[e] + apc * TV[e];
+    }
 #pragma unroll
     for (int t = 0; t < SI; ++t) {
       const int q = ul + TPB * t;
-      if (q < m) {
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
         const double sn = fmax(C.s[t] + apc * C.ds[t], 1e-8);
         const double zn = fmax(fmax(C.z[t] + adc * C.dz[t], 1e-8), 1e-8);
         C.s[t] = sn;
@@ -1592,9 +1600,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       }
     }
     // dy = the combined solve's dy (parked in RXu by refine_rhs) + the refinement's correction
-    for (int e = ul; e < p; e += TPB) {
-      const double dye = e < nx ? RXu[e] + QV[e] : DYm[e - nx];
-      Y[e] = Y[e] + adc * dye;
+#pragma unroll
+    for (int t = 0; t < (p + TPB - 1) / TPB; ++t) {
+      const int e = ul + TPB * t;
+      if (RegCtx<N>::full_slot(t, p) || e < p) {
+        const double dye = e < nx ? RXu[e] + QV[e] : DYm[e - nx];
+        Y[e] = Y[e] + adc * dye;
+      }
     }
     mu_new = C.block_sum(szn) / m;
     qp_sync<TPB>();
