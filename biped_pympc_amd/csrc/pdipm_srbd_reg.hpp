@@ -278,18 +278,31 @@ __device__ __forceinline__ double cel(const double* cc, int c, int b) {
   if (c >= 3 && c < 6 && b == c + 6) return cc[21 + c - 3];
   return 0.0;
 }
-// (M v)_r and (M^T v)_j from the compact block
-__device__ __forceinline__ double mrow(const double* mc, int r, const double* v) {
-  double a = mc[r] * v[r];
-  if (r < 3) a += (mc[12 + 3 * r] * v[6] + mc[13 + 3 * r] * v[7]) + mc[14 + 3 * r] * v[8];
-  else if (r < 6) a += mc[21 + r - 3] * v[r + 6];
-  return a;
+// (M v)_r and (M^T v)_j from the compact block. The row / column is lane-dependent, so the sparse
+// extra terms are formed in every lane from clamped indices and selected: nested divergent branches
+// (two exec-mask round trips each) cost more than the few FMAs
+// (M v)_r for the rows of equality slot t (RegCtx::erow): slot 0 holds r in {0,1,2,6,7,8}, where
+// rows 0..2 add the columns-6..8 block; slot 1 r in {3,4,5,9,10,11}, where rows 3..5 add (r, r + 6)
+template <int t>
+__device__ __forceinline__ double mrow_slot(const double* mc, int r, const double* v) {
+  const double a = mc[r] * v[r];
+  if constexpr (t == 0) {
+    const int rr = r < 3 ? r : 0;
+    const double x = (mc[12 + 3 * rr] * v[6] + mc[13 + 3 * rr] * v[7]) + mc[14 + 3 * rr] * v[8];
+    return r < 3 ? a + x : a;
+  } else {
+    const int rr = r < 6 ? r : 3;
+    const double x = mc[21 + rr - 3] * v[rr + 6];
+    return r < 6 ? a + x : a;
+  }
 }
 __device__ __forceinline__ double mcol(const double* mc, int j, const double* v) {
-  double a = mc[j] * v[j];
-  if (j >= 6 && j < 9) a += (mc[12 + j - 6] * v[0] + mc[15 + j - 6] * v[1]) + mc[18 + j - 6] * v[2];
-  else if (j >= 9) a += mc[21 + j - 9] * v[j - 6];
-  return a;
+  const double a = mc[j] * v[j];
+  const bool b6 = j >= 6 && j < 9, b9 = j >= 9;
+  const int j6 = b6 ? j - 6 : 0, j9 = b9 ? j - 9 : 0;
+  const double x6 = (mc[12 + j6] * v[0] + mc[15 + j6] * v[1]) + mc[18 + j6] * v[2];
+  const double x9 = mc[21 + j9] * v[j9 + 3];
+  return b6 ? a + x6 : (b9 ? a + x9 : a);
 }
 // dense 12-term row product (N block; rows are lane-dependent, so no per-row sparsity)
 __device__ __forceinline__ double drow12(const double* row, const double* v) {
@@ -447,7 +460,8 @@ struct RegCtx {
                           const double (&bv)[SE]) {
     const ERow q = erow(fresh_lane(), t);
     if (q.valid) {
-      double v = (q.i >= 1) ? mrow(Mc, q.r, X + 12 * (q.i - 1)) : 0.0;
+      const double mv = mrow_slot<t>(Mc, q.r, X + 12 * (q.i >= 1 ? q.i - 1 : 0));
+      double v = q.i >= 1 ? mv : 0.0;  // stage 0 has no previous stage
       v += Pd[q.r] * X[12 * q.i + q.r];
       v += nrow<t>(Nd, q.r, X + nx + 12 * q.i);
       re[t] = v - bv[t];
@@ -457,7 +471,8 @@ struct RegCtx {
   __device__ void g_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV) {
     const ERow q = erow(fresh_lane(), t);
     if (q.valid) {
-      double v = (q.i >= 1) ? mrow(Mc, q.r, TV + 12 * (q.i - 1)) : 0.0;
+      const double mv = mrow_slot<t>(Mc, q.r, TV + 12 * (q.i >= 1 ? q.i - 1 : 0));
+      double v = q.i >= 1 ? mv : 0.0;
       v += Pd[q.r] * TV[12 * q.i + q.r];
       v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
       QV[q.e] = v + re[t];
@@ -478,7 +493,8 @@ struct RegCtx {
         const int k = c / 12 + 1, j = c % 12;
         const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
-        if (k < N) ay += mcol(Mc, j, Y + 12 * k);
+        const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
+        ay = k < N ? ay + my : ay;
         rxx[t] = v + ay;
       }
     }
@@ -488,23 +504,22 @@ struct RegCtx {
       if (full_slot(t, nx) || c < nx) {
         const int i = c / 12, j = c % 12;
         const double v = Hu[j] * X[nx + c] + fu[t];
-        double gz = 0.0;
-        const int f = foot_of(j);
-        if (f >= 0) {
-          const int a = foot_pos(j);
-          const double* zf = Z + 16 * i + 8 * f;
-          const double* g = Gf + g_row(8 * f) + a;
-          double g0 = 0.0, g1 = 0.0;
+        // G^T z on the foot columns and the x-moment terms on columns 6 / 9, formed in every lane
+        // (clamped foot index) and selected
+        const int fj = foot_of(j), f = fj >= 0 ? fj : 0;
+        const double* zf = Z + 16 * i + 8 * f;
+        const double* g = Gf + g_row(8 * f) + foot_pos(j);
+        double g0 = 0.0, g1 = 0.0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            g0 += g[4 * k] * zf[k];
-            g1 += g[4 * (k + 4)] * zf[k + 4];
-          }
-          gz = g0 + g1;
+        for (int k = 0; k < 4; ++k) {
+          g0 += g[4 * k] * zf[k];
+          g1 += g[4 * (k + 4)] * zf[k + 4];
         }
+        const double gz = fj >= 0 ? g0 + g1 : 0.0;
         double ay = ncol(Nd, j, Y + 12 * i, j % 3);
-        if (j == 6) ay += SG[6] * Y[nx + 2 * i];
-        if (j == 9) ay += SG[7] * Y[nx + 2 * i + 1];
+        const bool e9 = j == 9;
+        const double ye = (e9 ? SG[7] : SG[6]) * Y[nx + 2 * i + (e9 ? 1 : 0)];
+        ay = (j == 6 || e9) ? ay + ye : ay;
         RXu[c] = (v + gz) + ay;
       }
     }
@@ -818,7 +833,8 @@ struct RegCtx {
                            double* DYs) {
     const ERow q = erow(fresh_lane(), t);
     if (q.valid) {
-      double v = (q.i >= 1) ? mrow(Mc, q.r, TV + 12 * (q.i - 1)) : 0.0;
+      const double mv = mrow_slot<t>(Mc, q.r, TV + 12 * (q.i >= 1 ? q.i - 1 : 0));
+      double v = q.i >= 1 ? mv : 0.0;
       v += Pd[q.r] * TV[12 * q.i + q.r];
       v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
       const double dy = QV[q.e];  // read and rewritten by its owner lane only
@@ -1076,7 +1092,8 @@ struct RegCtx {
       if (!kAffine && (full_slot(t, nx) || c < nx)) {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
-        if (k < N) aty += mcol(Mc, j, QV + 12 * k);
+        const double mq = mcol(Mc, j, QV + 12 * (k < N ? k : N - 1));  // k = N: unused
+        aty = k < N ? aty + mq : aty;
         TV[c] = TV[c] - aty * IX[j];
       }
     }
