@@ -444,9 +444,12 @@ struct RegCtx {
   // The lane index, re-materialised as an opaque value at the start of every phase: keeps the
   // compiler from hoisting each phase's per-lane addresses and predicates out of the Newton loop
   // (that alone pinned > 100 registers for the whole solve).
+  // Its upper bound stays known (l < TPB: guards of whole slots and lane ranges fold). Telling the
+  // compiler l >= 0 as well (unsigned index divisions) makes the fused N = 10 kernel spill 12 VGPRs.
   __device__ int fresh_lane() const {
     int l = lane;
     asm volatile("" : "+v"(l));
+    __builtin_assume(l < TPB);
     return l;
   }
   // Slot t of a row-parallel pass over n rows (row = lane + TPB t) lies wholly inside [0, n): its row
@@ -704,14 +707,17 @@ struct RegCtx {
     if (lane < 32) {
       const int g = lane >> 4, l16 = lane & 15;
       const int r = l16 < 12 ? l16 : 11;
-      const bool own = l16 < 12;
       const int pr = g ? perm12(r) : r;
       const int cnt = g ? nb : nf;
       const double* cc = at(Lo::Cc) + 24 * g;
+      // the coupling row's coefficients loaded from clamped indices and selected (a conditional
+      // load is an exec-mask round trip per coefficient)
       const double crd = cc[r];
-      const double cra0 = r < 3 ? cc[12 + 3 * r] : 0.0, cra1 = r < 3 ? cc[13 + 3 * r] : 0.0,
-                   cra2 = r < 3 ? cc[14 + 3 * r] : 0.0;
-      const double crb = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
+      const bool ra = r < 3, rb = r >= 3 && r < 6;
+      const int r3 = ra ? r : 0, r6 = rb ? r : 3;
+      const double la0 = cc[12 + 3 * r3], la1 = cc[13 + 3 * r3], la2 = cc[14 + 3 * r3], lb = cc[21 + r6 - 3];
+      const double cra0 = ra ? la0 : 0.0, cra1 = ra ? la1 : 0.0, cra2 = ra ? la2 : 0.0;
+      const double crb = rb ? lb : 0.0;
       uint32_t offs[12];  // byte offset of (pr, column c in group coordinates) in a step's blocks
       load_chain_offs(lane, offs);
       const CoupleRow Cr{crd, crb, cra0, cra1, cra2};
@@ -780,7 +786,7 @@ struct RegCtx {
           const double q = fwd_rhs(act, prev, mstep, g, r, Cr, wf, QV + 12 * i + pr);
           if (act && !(mstep && g == 1)) {
             wf = dot_bc12(Dr, q);
-            if (own) QV[12 * i + pr] = wf;
+            QV[12 * i + pr] = wf;  // shadow lanes 12..15 store row 11's value bit for bit
           }
         }
       }
@@ -1010,16 +1016,22 @@ struct RegCtx {
       CoupleRow Cr, Ct;  // row r of Cg and of Cg^T (compact layout, see the header)
       uint32_t offs[12];
       load_chain_offs(lane, offs);
-      Cr.d = cc[r];
-      Cr.b = (r >= 3 && r < 6) ? cc[21 + r - 3] : 0.0;
-      Cr.a0 = r < 3 ? cc[12 + 3 * r] : 0.0;
-      Cr.a1 = r < 3 ? cc[13 + 3 * r] : 0.0;
-      Cr.a2 = r < 3 ? cc[14 + 3 * r] : 0.0;
-      Ct.d = cc[r];
-      Ct.b = r >= 9 ? cc[12 + r] : 0.0;
-      Ct.a0 = (r >= 6 && r < 9) ? cc[12 + r - 6] : 0.0;
-      Ct.a1 = (r >= 6 && r < 9) ? cc[15 + r - 6] : 0.0;
-      Ct.a2 = (r >= 6 && r < 9) ? cc[18 + r - 6] : 0.0;
+      {  // coefficients loaded from clamped indices and selected (no conditional loads)
+        const bool ra = r < 3, rb = r >= 3 && r < 6, ta = r >= 6 && r < 9, tb = r >= 9;
+        const int r3 = ra ? r : 0, r6 = rb ? r : 3, t6 = ta ? r : 6, t9 = tb ? r : 9;
+        const double la0 = cc[12 + 3 * r3], la1 = cc[13 + 3 * r3], la2 = cc[14 + 3 * r3], lb = cc[21 + r6 - 3];
+        const double ka0 = cc[12 + t6 - 6], ka1 = cc[15 + t6 - 6], ka2 = cc[18 + t6 - 6], kb = cc[12 + t9];
+        Cr.d = cc[r];
+        Cr.b = rb ? lb : 0.0;
+        Cr.a0 = ra ? la0 : 0.0;
+        Cr.a1 = ra ? la1 : 0.0;
+        Cr.a2 = ra ? la2 : 0.0;
+        Ct.d = Cr.d;
+        Ct.b = tb ? kb : 0.0;
+        Ct.a0 = ta ? ka0 : 0.0;
+        Ct.a1 = ta ? ka1 : 0.0;
+        Ct.a2 = ta ? ka2 : 0.0;
+      }
       double w = 0.0, wv[T + 1];  // w / v per elimination step, indexed through selects
 #pragma unroll
       for (int k = 0; k <= T; ++k) wv[k] = 0.0;
