@@ -75,7 +75,8 @@ struct RegLayout {
                        Z = X + nz, Y = Z + m, RXu = Y + p, VV = RXu + nx, TV = VV + m,
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
                        RED = DYm + 2 * N,  // block reductions of a multi-wave QP: 2 slot sets
-                       end = RED + (TPB > 64 ? 2 * (TPB / 64) : 0),
+                       DMY = RED + (TPB > 64 ? 2 * (TPB / 64) : 0),  // sink of the invalid lanes' stores
+                       end = DMY + 2,
                        // the fused prologue's FormerLds scratch from TV on (pads the short horizons)
                        former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16),
                        total = end > former ? end : former;
@@ -279,8 +280,9 @@ __device__ __forceinline__ double cel(const double* cc, int c, int b) {
   return 0.0;
 }
 // (M v)_r and (M^T v)_j from the compact block. The row / column is lane-dependent, so the sparse
-// extra terms are formed in every lane from clamped indices and selected: nested divergent branches
-// (two exec-mask round trips each) cost more than the few FMAs
+// extra terms are formed in every lane from clamped indices and added with a 0 / 1 weight (fma(w, x,
+// a) is a + x or a exactly): nested divergent branches (two exec-mask round trips each) cost more
+// than the few FMAs, and a select would let the compiler sink the loads back into branches
 // (M v)_r for the rows of equality slot t (RegCtx::erow): slot 0 holds r in {0,1,2,6,7,8}, where
 // rows 0..2 add the columns-6..8 block; slot 1 r in {3,4,5,9,10,11}, where rows 3..5 add (r, r + 6)
 template <int t>
@@ -289,11 +291,11 @@ __device__ __forceinline__ double mrow_slot(const double* mc, int r, const doubl
   if constexpr (t == 0) {
     const int rr = r < 3 ? r : 0;
     const double x = (mc[12 + 3 * rr] * v[6] + mc[13 + 3 * rr] * v[7]) + mc[14 + 3 * rr] * v[8];
-    return r < 3 ? a + x : a;
+    return fma(r < 3 ? 1.0 : 0.0, x, a);
   } else {
     const int rr = r < 6 ? r : 3;
     const double x = mc[21 + rr - 3] * v[rr + 6];
-    return r < 6 ? a + x : a;
+    return fma(r < 6 ? 1.0 : 0.0, x, a);
   }
 }
 __device__ __forceinline__ double mcol(const double* mc, int j, const double* v) {
@@ -302,7 +304,7 @@ __device__ __forceinline__ double mcol(const double* mc, int j, const double* v)
   const int j6 = b6 ? j - 6 : 0, j9 = b9 ? j - 9 : 0;
   const double x6 = (mc[12 + j6] * v[0] + mc[15 + j6] * v[1]) + mc[18 + j6] * v[2];
   const double x9 = mc[21 + j9] * v[j9 + 3];
-  return b6 ? a + x6 : (b9 ? a + x9 : a);
+  return fma(b9 ? 1.0 : 0.0, x9, fma(b6 ? 1.0 : 0.0, x6, a));
 }
 // dense 12-term row product (N block; rows are lane-dependent, so no per-row sparsity)
 __device__ __forceinline__ double drow12(const double* row, const double* v) {
@@ -458,28 +460,30 @@ struct RegCtx {
   __device__ static constexpr bool full_slot(int t, int n) { return TPB * (t + 1) <= n; }
 
   // --------------------------------------------------------------------- residuals ----
+  // Equality-row slots run in every lane: a lane past the slot's rows (q.valid false) computes on
+  // in-bounds LDS rows of a stage past the horizon, keeps the result in its own re[t] (read only
+  // under q.valid) and stores to the DMY sink -- no divergent branch around the phase.
+  // (A v)_r of one dynamics row: M v_{i-1} (stage 0 has none: weight 0) + P v_i + N u_i
+  template <int t>
+  __device__ double arow(const double* V, const double* Mc, const double* Pd, const double* Nd, const ERow& q) const {
+    const double mv = mrow_slot<t>(Mc, q.r, V + 12 * (q.i >= 1 ? q.i - 1 : 0));
+    double v = (q.i >= 1 ? 1.0 : 0.0) * mv;
+    v += Pd[q.r] * V[12 * q.i + q.r];
+    v += nrow<t>(Nd, q.r, V + nx + 12 * q.i);
+    return v;
+  }
+  // index into the vector at L + base of row e, or the DMY sink for an invalid lane
+  __device__ static int sink(bool valid, int e, int base) { return valid ? e : Lo::DMY - base; }
   template <int t>
   __device__ void re_slot(const double* X, const double* Mc, const double* Pd, const double* Nd,
                           const double (&bv)[SE]) {
     const ERow q = erow(fresh_lane(), t);
-    if (q.valid) {
-      const double mv = mrow_slot<t>(Mc, q.r, X + 12 * (q.i >= 1 ? q.i - 1 : 0));
-      double v = q.i >= 1 ? mv : 0.0;  // stage 0 has no previous stage
-      v += Pd[q.r] * X[12 * q.i + q.r];
-      v += nrow<t>(Nd, q.r, X + nx + 12 * q.i);
-      re[t] = v - bv[t];
-    }
+    re[t] = arow<t>(X, Mc, Pd, Nd, q) - bv[t];
   }
   template <int t>
   __device__ void g_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV) {
     const ERow q = erow(fresh_lane(), t);
-    if (q.valid) {
-      const double mv = mrow_slot<t>(Mc, q.r, TV + 12 * (q.i >= 1 ? q.i - 1 : 0));
-      double v = q.i >= 1 ? mv : 0.0;
-      v += Pd[q.r] * TV[12 * q.i + q.r];
-      v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
-      QV[q.e] = v + re[t];
-    }
+    QV[sink(q.valid, q.e, Lo::QV)] = arow<t>(TV, Mc, Pd, Nd, q) + re[t];
   }
   // want_mu (wave-uniform): also return mu = s^T z / m -- the first iteration only: afterwards it
   // equals the previous iteration's mu_new, the same products s_t z_t summed in the same order
@@ -497,7 +501,7 @@ struct RegCtx {
         const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
-        ay = k < N ? ay + my : ay;
+        ay = fma(k < N ? 1.0 : 0.0, my, ay);
         rxx[t] = v + ay;
       }
     }
@@ -518,11 +522,11 @@ struct RegCtx {
           g0 += g[4 * k] * zf[k];
           g1 += g[4 * (k + 4)] * zf[k + 4];
         }
-        const double gz = fj >= 0 ? g0 + g1 : 0.0;
+        const double gz = (fj >= 0 ? 1.0 : 0.0) * (g0 + g1);
         double ay = ncol(Nd, j, Y + 12 * i, j % 3);
         const bool e9 = j == 9;
-        const double ye = (e9 ? SG[7] : SG[6]) * Y[nx + 2 * i + (e9 ? 1 : 0)];
-        ay = (j == 6 || e9) ? ay + ye : ay;
+        const double se = (j == 6 || e9) ? 1.0 : 0.0;
+        ay = fma(se * (e9 ? SG[7] : SG[6]), Y[nx + 2 * i + (e9 ? 1 : 0)], ay);
         RXu[c] = (v + gz) + ay;
       }
     }
@@ -838,15 +842,11 @@ struct RegCtx {
   __device__ void rho_slot(const double* TV, const double* Mc, const double* Pd, const double* Nd, double* QV,
                            double* DYs) {
     const ERow q = erow(fresh_lane(), t);
-    if (q.valid) {
-      const double mv = mrow_slot<t>(Mc, q.r, TV + 12 * (q.i >= 1 ? q.i - 1 : 0));
-      double v = q.i >= 1 ? mv : 0.0;
-      v += Pd[q.r] * TV[12 * q.i + q.r];
-      v += nrow<t>(Nd, q.r, TV + nx + 12 * q.i);
-      const double dy = QV[q.e];  // read and rewritten by its owner lane only
-      if (kPark) DYs[q.e] = dy;
-      QV[q.e] = (v + re[t]) - kDelta * dy;
-    }
+    const double v = arow<t>(TV, Mc, Pd, Nd, q);
+    const int e = sink(q.valid, q.e, Lo::QV);
+    const double dy = QV[e];  // read and rewritten by its owner lane only
+    if (kPark) DYs[sink(q.valid, q.e, Lo::RXu)] = dy;
+    QV[e] = (v + re[t]) - kDelta * dy;
   }
   // kAff: the affine (predictor) direction at a degenerate iterate (see the main loop): r_s stays
   // (the combined solve needs it), e3 goes to Z for solve_finish<true, true>, and dy is not parked
@@ -1105,7 +1105,7 @@ struct RegCtx {
         const int k = c / 12 + 1, j = c % 12;
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         const double mq = mcol(Mc, j, QV + 12 * (k < N ? k : N - 1));  // k = N: unused
-        aty = k < N ? aty + mq : aty;
+        aty = fma(k < N ? 1.0 : 0.0, mq, aty);
         TV[c] = TV[c] - aty * IX[j];
       }
     }
