@@ -372,7 +372,7 @@ struct RegCtx {
       return q;
     }
     q.valid = l < 6 * N;
-    q.i = l / 6;
+    q.i = (int)((unsigned)l / 6u);  // l >= 0: unsigned division (no sign fix-up)
     const int k = l - 6 * q.i;
     q.r = t == 0 ? (k < 3 ? k : k + 3) : (k < 3 ? k + 3 : k + 6);
     q.e = 12 * q.i + q.r;
@@ -497,7 +497,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
-        const int k = c / 12 + 1, j = c % 12;
+        const int k = (int)((unsigned)c / 12u) + 1, j = (int)((unsigned)c % 12u);
         const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
@@ -509,7 +509,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // r_x, u columns: H_u u + f + G^T z + N^T y + e-rows (LDS)
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
-        const int i = c / 12, j = c % 12;
+        const int i = (int)((unsigned)c / 12u), j = (int)((unsigned)c % 12u);
         const double v = Hu[j] * X[nx + c] + fu[t];
         // G^T z on the foot columns and the x-moment terms on columns 6 / 9, formed in every lane
         // (clamped foot index) and selected
@@ -545,7 +545,7 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) {  // r_s = G u + s - h (owner regs)
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
-        const int i = q / 16, k = q % 16;
+        const int i = q >> 4, k = q & 15;
         const double v = grow4(Gf, k, X + nx + 12 * i);
         rs[t] = (v + s[t]) - hv[t];
         sz += s[t] * z[t];
@@ -863,7 +863,7 @@ struct RegCtx {
         const int q = lane + TPB * t;
         e3r[t] = 0.0;
         if (RegCtx<N>::full_slot(t, m) || q < m) {
-          const int i = q / 16, k = q % 16;
+          const int i = q >> 4, k = q & 15;
           const double gd = grow4(Gf, k, TV + nx + 12 * i);
           const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
           const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
@@ -948,7 +948,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
       const int c = lane + TPB * t;
-      if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[c % 12];
+      if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[(unsigned)c % 12u];
     }
     qp_sync<TPB>();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
@@ -1102,7 +1102,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int c = lane + TPB * t;
       if (!kAffine && (full_slot(t, nx) || c < nx)) {
-        const int k = c / 12 + 1, j = c % 12;
+        const int k = (int)((unsigned)c / 12u) + 1, j = (int)((unsigned)c % 12u);
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         const double mq = mcol(Mc, j, QV + 12 * (k < N ? k : N - 1));  // k = N: unused
         aty = fma(k < N ? 1.0 : 0.0, mq, aty);
@@ -1151,7 +1151,7 @@ struct RegCtx {
     for (int t = 0; t < SI; ++t) {  // dz, ds (owner regs)
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
-        const int i = q / 16, k = q % 16;
+        const int i = q >> 4, k = q & 15;
         const double gd = grow4(Gf, k, TV + nx + 12 * i);
         const double vq = VV[q];
         dz[t] = vq + di[t] * wd[t] * gd;
