@@ -86,6 +86,15 @@ struct RegLayout {
   static_assert((DV & 1) == 0 && (X & 1) == 0 && (TV & 1) == 0, "16-byte aligned vectors");
 };
 
+// Index arithmetic on lane-derived values (non-negative, far below 2^16) through the full-rate
+// 24-bit multiplier: the compiler cannot bound an opaque lane to 24 bits, so it emits the
+// quarter-rate v_mul_lo_u32 / v_mul_hi_u32 for c / 12, 12 i and the like.
+__device__ __forceinline__ int m24(int a, int b) { return (int)__umul24((unsigned)a, (unsigned)b); }
+// c / 12 and c / 6 by reciprocal multiplication: 43691 * 12 = 2^19 + 4, exact for 0 <= c < 2^17
+// (c / 6: < 2^16, where the product also stays below 2^32)
+__device__ __forceinline__ int div12(int c) { return (int)(__umul24((unsigned)c, 43691u) >> 19); }
+__device__ __forceinline__ int div6(int c) { return (int)(__umul24((unsigned)c, 43691u) >> 18); }
+
 // foot of u column j ({0,1,2,7} left, {3,4,5,10} right, else -1), its position, and the inverse
 __device__ __forceinline__ int foot_of(int j) { return (j < 3 || j == 7) ? 0 : ((j < 6 || j == 10) ? 1 : -1); }
 __device__ __forceinline__ int foot_pos(int j) { return j < 6 ? j % 3 : 3; }
@@ -372,10 +381,10 @@ struct RegCtx {
       return q;
     }
     q.valid = l < 6 * N;
-    q.i = (int)((unsigned)l / 6u);  // l >= 0: unsigned division (no sign fix-up)
-    const int k = l - 6 * q.i;
+    q.i = div6(l);
+    const int k = l - m24(q.i, 6);
     q.r = t == 0 ? (k < 3 ? k : k + 3) : (k < 3 ? k + 3 : k + 6);
-    q.e = 12 * q.i + q.r;
+    q.e = m24(q.i, 12) + q.r;
     return q;
   }
   // (N u)_r of stage i's u block for a slot-t row (slot 1: the two force columns of row r)
@@ -497,7 +506,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // r_x, x columns: H_x x + f + P y_{k-1} + M^T y_k (owner regs)
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
-        const int k = (int)((unsigned)c / 12u) + 1, j = (int)((unsigned)c % 12u);
+        const int k = div12(c) + 1, j = c - m24(k - 1, 12);
         const double v = Hu[12 + j] * X[c] + fx[t];
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
@@ -509,7 +518,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // r_x, u columns: H_u u + f + G^T z + N^T y + e-rows (LDS)
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
-        const int i = (int)((unsigned)c / 12u), j = (int)((unsigned)c % 12u);
+        const int i = div12(c), j = c - m24(i, 12);
         const double v = Hu[j] * X[nx + c] + fu[t];
         // G^T z on the foot columns and the x-moment terms on columns 6 / 9, formed in every lane
         // (clamped foot index) and selected
@@ -546,7 +555,7 @@ struct RegCtx {
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q >> 4, k = q & 15;
-        const double v = grow4(Gf, k, X + nx + 12 * i);
+        const double v = grow4(Gf, k, X + nx + m24(i, 12));
         rs[t] = (v + s[t]) - hv[t];
         sz += s[t] * z[t];
       }
@@ -864,7 +873,7 @@ struct RegCtx {
         e3r[t] = 0.0;
         if (RegCtx<N>::full_slot(t, m) || q < m) {
           const int i = q >> 4, k = q & 15;
-          const double gd = grow4(Gf, k, TV + nx + 12 * i);
+          const double gd = grow4(Gf, k, TV + nx + m24(i, 12));
           const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
           const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
           const double qc = di[t] * (e2 - wd[t] * e3);
@@ -948,7 +957,7 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < SX; ++t) {
       const int c = lane + TPB * t;
-      if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[(unsigned)c % 12u];
+      if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[c - m24(div12(c), 12)];
     }
     qp_sync<TPB>();
     // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
@@ -1102,7 +1111,7 @@ struct RegCtx {
     for (int t = 0; t < SX; ++t) {  // dx (x part) = t - phi_x^-1 A^T dy
       const int c = lane + TPB * t;
       if (!kAffine && (full_slot(t, nx) || c < nx)) {
-        const int k = (int)((unsigned)c / 12u) + 1, j = (int)((unsigned)c % 12u);
+        const int k = div12(c) + 1, j = c - m24(k - 1, 12);
         double aty = Pd[j] * QV[12 * (k - 1) + j];
         const double mq = mcol(Mc, j, QV + 12 * (k < N ? k : N - 1));  // k = N: unused
         aty = fma(k < N ? 1.0 : 0.0, mq, aty);
@@ -1152,7 +1161,7 @@ struct RegCtx {
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q >> 4, k = q & 15;
-        const double gd = grow4(Gf, k, TV + nx + 12 * i);
+        const double gd = grow4(Gf, k, TV + nx + m24(i, 12));
         const double vq = VV[q];
         dz[t] = vq + di[t] * wd[t] * gd;
         // the affine refinement keeps r_s and parks its row-3 residual e3 in Z (refine_rhs<true>)
