@@ -7,8 +7,12 @@ caller's QP step (biped_pympc/convex_mpc/mpc_controller_cusadi.py:99-169) at BAS
 4096-env shard (weak scaling) and the first-stage inputs u0 (12 doubles/env, the only thing the
 wrapper consumes, mpc_controller_cusadi.py:186) are gathered over RCCL.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]   (multi-GPU via torch.distributed.run)
-Prints ONE JSON line on rank 0.
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  --gpus N > 1 without an external launcher: this process starts N ranks itself (one child process
+  per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+  environment), touches no GPU itself, and exits with the first failing rank's status. Under
+  torch.distributed.run (WORLD_SIZE set) --gpus must equal WORLD_SIZE, else it exits 2.
+Prints ONE JSON line on rank 0; n_gpus = the ranks that joined the process group.
 """
 from __future__ import annotations
 
@@ -25,7 +29,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from biped_pympc_amd import solver  # noqa: E402
+from biped_pympc_amd import _native, solver  # noqa: E402
 from biped_pympc_amd.layout import Dims  # noqa: E402
 from biped_pympc_amd.sharding import ShardedMPC  # noqa: E402
 from biped_pympc_amd.utils.synthetic import make_workload  # noqa: E402
@@ -44,9 +48,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 NODE_GPUS = int(os.environ.get("SRBD_NODE_GPUS", "8"))  # GPUs sharing one host (an 8-GPU MI355X node)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); > 1 without WORLD_SIZE set: bench.py starts them itself")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch-per-gpu", type=int, default=4096)
@@ -60,7 +65,78 @@ def parse():
                    help="also time the CPU baseline on every CPU the process may run on (off by default: "
                         "the GPU box gives one GPU's job a 16-CPU share of the host)")
     p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
-    return p.parse_args()
+    p.add_argument("--no-dropin", action="store_true",
+                   help="skip the reference caller's CusADi schedule leg (1 former + 4 x 5-iteration evaluate)")
+    p.add_argument("--dump-u0", default=None,
+                   help="rank 0 saves the gathered u0 (global env order) of the last timed step as .npy")
+    return p.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv) -> int:
+    """Start a.gpus ranks of this script (one process per GPU) and wait for them.
+
+    The parent imports nothing that touches the GPU and never execs: each rank is a child process
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run
+    would set them. Rank 0's stdout (the JSON line) is this process's stdout; the other ranks'
+    stdout is dropped, every rank's stderr is kept. If a rank fails, the others are terminated
+    (a rank left waiting in a collective would otherwise hang) and its exit status is returned."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = {s: signal.signal(s, lambda *x, s=s: (stop(), sys.exit(128 + s))) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            for r, p in enumerate(procs):
+                code = p.poll()
+                if code not in (None, 0) and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {r} exited with status {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    stop()
+            time.sleep(0.1)
+        for r, p in enumerate(procs):
+            if p.returncode not in (0, None) and rc == 0:
+                rc = p.returncode if p.returncode > 0 else 128 - p.returncode
+    finally:
+        stop()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
+def load_solve_hook(spec: str):
+    """SRBD_BENCH_SOLVE_HOOK="module:factory" -- test hook (never set by the driver): the step's
+    solve becomes factory(N, K)(local_inputs) -> x on the CPU and every GPU leg is skipped, so the
+    launcher, the process group and the u0 gather run on a machine without a GPU (tests/)."""
+    import importlib
+    mod, _, attr = spec.partition(":")
+    return getattr(importlib.import_module(mod), attr)
 
 
 def event_time_ms(fn, reps: int, warm: int = 2) -> float:
@@ -131,6 +207,15 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup v2 CPU controller (cpu.max "quota period"), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
 def _physical_cores(cpus) -> int:
     """Distinct (package, core) pairs among the logical CPUs `cpus` (SMT siblings count once)."""
     seen = set()
@@ -144,30 +229,160 @@ def _physical_cores(cpus) -> int:
     return len(seen)
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def run_timed(sh, inputs, a, dist, world, dev):
+    """W untimed warm-up steps, then EXACTLY a.steps steps bracketed by a barrier + device sync on
+    both sides; returns (max over ranks of the elapsed seconds, u0 of every env after the last step).
+    At world > 1 each step leaves its u0 gather running on the collective's stream (overlapping the
+    next step's solve) and every gather completes inside the timed region."""
+    cuda = dev.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    pending = []
+    last = [None]
+
+    def step():
+        if world == 1:
+            last[0] = sh.step(inputs)  # fused former + PDIPM
+        else:
+            pending.append(sh.step_async(inputs))
+
+    def drain():
+        for h in pending:
+            last[0] = h.wait()
+        pending.clear()
+
+    for _ in range(a.warmup):
+        step()
+    drain()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    drain()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, last[0]
+
+
+def hook_main(a, hook, dist, world, rank, N, K, B, d):
+    """The launcher / process-group / gather path with a CPU solve (SRBD_BENCH_SOLVE_HOOK): same
+    workload seeds and timing as main(), no GPU leg; the line says which solve ran."""
+    dev = torch.device("cpu")
+    wl = make_workload(B, N, seed=1000 + rank, random_gait=a.random_gait)
+    inputs = [torch.from_numpy(x) for x in wl.inputs]
+    sh = ShardedMPC(N, K, world * B, device=dev, y0=1.0, solve_fn=load_solve_hook(hook)(N, K))
+    elapsed, u0_last = run_timed(sh, inputs, a, dist, world, dev)
+    if rank == 0:
+        if a.dump_u0:
+            np.save(a.dump_u0, u0_last.numpy())
+        emit({
+            "metric": f"batched SRBD QP solves/sec (N={N}, {K} PDIPM iters)", "value": round(world * B * a.steps / elapsed, 1),
+            "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"CPU solve hook {hook} (launcher test; not a GPU measurement)",
+                       "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "pdipm_iters": K,
+                       "parallelism": f"dp{world}" + (" (u0 all_gather over gloo)" if world > 1 else "")}})
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _claim_stdout():
+    """The JSON line is the only thing on stdout: native libraries (gloo, RCCL, HIP) print
+    diagnostics to file descriptor 1, so fd 1 is pointed at stderr and the line goes to a private
+    duplicate of the original stdout."""
+    global OUT
+    sys.stdout.flush()
+    OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+OUT = sys.stdout
+
+
+def emit(line: dict) -> None:
+    print(json.dumps(line), file=OUT, flush=True)
+
+
+def dropin_leg(inputs, N: int, B: int, reps: int) -> dict:
+    """The reference caller's own schedule through the CusADi-ABI drop-in libraries
+    (mpc_controller_cusadi.py:99-172: 1 former evaluate, 4 x 5-iteration solver evaluate, blocking,
+    with the dense rebuilds and clones between calls), timed on the host clock because every
+    evaluate blocks, beside the one-launch fused step with the same 20 iterations."""
+    from biped_pympc_amd.cusadi.reference_step import ReferenceQPSchedule
+    out = {}
+    xs = {}
+    for name, lean in (("literal", False), ("lean", True)):
+        sched = ReferenceQPSchedule(N, B, lean=lean)
+        xs[name] = sched.run(inputs)  # warm: library load, attribute setup
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(max(2, reps // 2)):
+            sched.run(inputs)
+        torch.cuda.synchronize()
+        out[f"{name}_ms"] = round(1e3 * (time.perf_counter() - t0) / max(2, reps // 2), 4)
+        del sched
+    bufs = solver.MPCSolveBuffers.allocate(N, B, inputs[0].device)
+    out["fused_k20_ms"] = round(event_time_ms(lambda: solver.mpc_solve(inputs, N, 20, 1.0, buffers=bufs), reps), 4)
+    x20 = bufs.outputs[0]
+    for name, x in xs.items():
+        out[f"{name}_vs_fused_max_rel"] = float(((x - x20).abs().amax(dim=1) / x20.abs().amax(dim=1)).max())
+    out["note"] = ("MPCControllerCusadi.run's QP schedule (INTEGRATION.md option A): 1 former + 4 x 5-iteration "
+                   "evaluate, blocking, through CusadiFunction; 'literal' keeps the reference's dense "
+                   "getDenseOutput rebuilds, bmm init and clones, 'lean' feeds the sparse outputs back; "
+                   "fused_k20 = the same 20 Newton iterations as one srbd_mpc_solve_fused launch")
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a, argv))  # this process only starts and joins the ranks
+    _claim_stdout()
+    world = int(env_world or "1")
+    if a.gpus < 1 or world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} ranks were launched", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    hook = os.environ.get("SRBD_BENCH_SOLVE_HOOK")
     # rehearsal hooks for the N > 1 path on a one-GPU box (never set by the driver): all ranks on
     # device 0, and gloo instead of RCCL (RCCL rejects two ranks on one device)
     one_device = os.environ.get("SRBD_BENCH_ONE_DEVICE") == "1"
-    backend = os.environ.get("SRBD_BENCH_BACKEND", "nccl")
+    backend = "gloo" if hook else os.environ.get("SRBD_BENCH_BACKEND", "nccl")
     if one_device:
         local = 0
+    if not hook and local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist_mod
         dist = dist_mod
-        torch.cuda.set_device(local)
         if backend == "nccl":
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+        world = dist.get_world_size()  # n_gpus = the ranks that joined
+        rank = dist.get_rank()
     N, K, B = a.horizon, a.iters, a.batch_per_gpu
     d = Dims(N)
+    if hook:
+        return hook_main(a, hook, dist, world, rank, N, K, B, d)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
 
     # each rank's shard of the global synthetic batch (world x B robots) is generated locally
     wl = make_workload(B, N, seed=1000 + rank, random_gait=a.random_gait)
@@ -188,40 +403,11 @@ def main():
     ms_fused = event_time_ms(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), a.kernel_reps)
     del pd_out
 
-    pending = []
-
-    def step():
-        if world == 1:
-            return sh.step(inputs)  # fused former + PDIPM
-        # shard solve; the u0 gather (RCCL) runs on its own stream, overlapping the next step
-        pending.append(sh.step_async(inputs))
-
-    def drain():  # every gather of the timed steps completes inside the timed region
-        for h in pending:
-            h.wait()
-        pending.clear()
-
-    for _ in range(a.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, u0_last = run_timed(sh, inputs, a, dist, world, dev)
     ms_step = 1e3 * elapsed / a.steps
     value = world * B * a.steps / elapsed
+    if rank == 0 and a.dump_u0:
+        np.save(a.dump_u0, u0_last.cpu().numpy())
 
     # the step's kernel timed again at steady clocks (the legs above also serve as the clock warm-up);
     # roofline.achieved uses this figure
@@ -249,6 +435,9 @@ def main():
         m1, m3 = ab(c256)
         ctrl["b256"] = {"one_launch_ms": round(m1, 4), "three_kernel_ms": round(m3, 4)}
         del c, c256
+    dropin = None
+    if rank == 0 and not a.no_dropin:
+        dropin = dropin_leg(inputs, N, B, a.kernel_reps)
     ms_gather = None
     if dist is not None:
         u0 = bufs.outputs[0][:, 12 * N:12 * N + 12]
@@ -307,8 +496,28 @@ def main():
         phys_host = _physical_cores(range(host_cpus))
         phys_aff = _physical_cores(aff_cpus)
         cores_used = min(threads, phys_aff)  # OpenMP threads spread over distinct physical cores first
+        quota = _cgroup_cpu_quota()
+        # thread scaling inside the process's CPU share (1 .. threads, ~1 s each): the evidence for
+        # (or against) the linear per-core extrapolation to the whole host below
+        scaling = {}
+        t_ = 1
+        while t_ <= threads:
+            oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=t_)
+            ns, ts = 0, 0.0
+            while ts < 1.0:
+                t1 = time.perf_counter()
+                oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=t_)
+                ts += time.perf_counter() - t1
+                ns += sample
+            scaling[str(t_)] = round(ns / ts, 1)
+            t_ = t_ * 2 if t_ * 2 <= threads or t_ == threads else threads
         full = None
-        if a.cpu_full_host:  # measured on every CPU of the affinity set (opt-in, see --help)
+        if quota is not None and quota < affinity:
+            # the CPU controller caps this process at `quota` CPUs whatever its affinity: a run with
+            # every CPU of the affinity set would time the quota, not the host
+            full = {"value": None, "reason": f"cgroup cpu.max allows {quota:g} CPUs of the {affinity} in the "
+                                             f"affinity set: the whole host cannot be timed from this process"}
+        if a.cpu_full_host and full is None:  # measured on every CPU of the affinity set (opt-in)
             oracle.mpc_solve(N, K, sub, y0=1.0, nthreads=affinity)
             nf, tf = 0, 0.0
             while tf < a.cpu_seconds / 2:
@@ -341,7 +550,8 @@ def main():
                         "per_gpu_share_estimate": round(solves / t_cpu / cores_used * phys_host / NODE_GPUS, 1),
                         "node_gpus": NODE_GPUS,
                         "full_host_estimate": round(solves / t_cpu / cores_used * phys_host, 1),
-                        "full_host_measured": full},
+                        "full_host_measured": full, "cgroup_cpu_quota": quota,
+                        "thread_scaling_solves_per_s": scaling},
                "sample": (f"C oracle (full-KKT sparse LDL^T PDIPM, OpenMP over envs, {threads} threads) on "
                           f"the first {sample} envs of the same workload, {solves // sample} passes, "
                           f"{t_cpu:.1f} s, N={N}, {K} iterations"),
@@ -382,12 +592,14 @@ def main():
             "kernels_ms": {"mpc_step_fused": round(ms_fused, 4) if fused else None,
                            "qp_former": round(ms_former, 4), "pdipm": round(ms_pdipm, 4),
                            "u0_all_gather": None if ms_gather is None else round(ms_gather, 4)},
+            "build_id": _native.build_id(),  # source hash libsrbd_mpc.so was built from (build.py)
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
             "controller_step": ctrl,
+            "dropin_step": dropin,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -35,8 +35,11 @@ def lib() -> ctypes.CDLL:
             f"{path} not found: build it with `python -m biped_pympc_amd.build` (hipcc, gfx950). "
             "There is no CPU fallback for the SRBD-MPC kernels.")
     L = ctypes.CDLL(path)
+    if os.environ.get("SRBD_LIB"):  # an earlier build (A/B runs): bind what it exports
+        L = _Tolerant(L)
     L.srbd_abi_version.restype = ctypes.c_int
     L.srbd_last_error.restype = ctypes.c_char_p
+    L.srbd_build_id.restype = ctypes.c_char_p
     L.srbd_solver_lds_bytes.restype = ctypes.c_size_t
     L.srbd_solver_lds_bytes.argtypes = [ctypes.c_int]
     L.srbd_mpc_workspace_doubles.restype = ctypes.c_size_t
@@ -56,6 +59,14 @@ def lib() -> ctypes.CDLL:
                                  ctypes.c_void_p, P, ctypes.c_void_p]
     L.srbd_mpc_solve_fused.restype = ctypes.c_int
     L.srbd_mpc_solve_fused.argtypes = L.srbd_mpc_solve.argtypes
+    L.srbd_mpc_solve_fused_ex.restype = ctypes.c_int
+    L.srbd_mpc_solve_fused_ex.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
+                                          ctypes.c_void_p, P, _c_dp, ctypes.c_void_p]
+    L.srbd_pdipm_ex.restype = ctypes.c_int
+    L.srbd_pdipm_ex.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P,
+                                _c_dp, ctypes.c_void_p]
+    L.srbd_prepare_device.restype = ctypes.c_int
+    L.srbd_prepare_device.argtypes = []
     L.srbd_evaluate_qp_former.restype = ctypes.c_float
     L.srbd_evaluate_qp_former.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]
@@ -74,6 +85,8 @@ def lib() -> ctypes.CDLL:
     L.srbd_mpc_step.restype = ctypes.c_int
     L.srbd_mpc_step.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(MPCPrep),
                                 P, P, _c_dp, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
+    L.srbd_mpc_step_ex.restype = ctypes.c_int
+    L.srbd_mpc_step_ex.argtypes = L.srbd_mpc_step.argtypes[:-1] + [_c_dp, ctypes.c_void_p]
     L.srbd_u0_wrench.restype = ctypes.c_int
     L.srbd_u0_wrench.argtypes = [ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_void_p]
     L.srbd_u0_wrench_torque.restype = ctypes.c_int
@@ -84,6 +97,29 @@ def lib() -> ctypes.CDLL:
                                      ctypes.c_void_p]
     _lib = L
     return L
+
+
+class _Tolerant:
+    """A library handle whose missing symbols bind to a stub raising on call (SRBD_LIB pointing at a
+    build from an earlier tree, for scripts/ab_bench.sh)."""
+
+    class _Missing:
+        def __init__(self, name):
+            self.name = name
+
+        def __call__(self, *a):
+            raise NativeLibraryMissing(f"{self.name} is not exported by {lib_path()}")
+
+    def __init__(self, L):
+        object.__setattr__(self, "_L", L)
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._L, name)
+        except AttributeError:
+            stub = _Tolerant._Missing(name)
+            object.__setattr__(self, name, stub)
+            return stub
 
 
 class MPCPrep(ctypes.Structure):
@@ -111,6 +147,9 @@ def check(rc: int, what: str) -> None:
 
 SOLVER_PATHS = {"auto": 0, "general": 1, "lds": 2}
 
+# per-problem status word bits (include/srbd_mpc.h SRBD_STATUS_*)
+STATUS_NONFINITE, STATUS_STEP_FLOOR, STATUS_FALLBACK = 1, 2, 4
+
 
 def current_solver_path() -> int:
     """Solver path code in effect for the current HIP device (0 = auto)."""
@@ -119,10 +158,11 @@ def current_solver_path() -> int:
 
 class solver_path:
     """Context manager selecting the solver kernels: "auto" (stage-invariant kernels -- the
-    register-resident one at N = 10 and 20 -- plus the general fallback), "general" (general kernel only)
-    or "lds" (the LDS-resident stage-invariant kernel at every horizon). For the HIP device current
-    on entry; on exit the previous path of that device is restored. For tests/benchmarks.
-    ``srbd_mpc_step`` (the one-launch controller step) ignores the path."""
+    register-resident ones at N = 2..32, the LDS-resident one at N = 1 -- plus the in-launch general
+    fallback for a QP that is not stage-invariant), "general" (general kernel only) or "lds" (the
+    LDS-resident stage-invariant kernel at every horizon). For the HIP device current on entry; on exit
+    the previous path of that device is restored. For tests/benchmarks. ``srbd_mpc_step`` (the
+    one-launch controller step) ignores the path."""
 
     def __init__(self, path: str):
         self.code = SOLVER_PATHS[path]
@@ -140,6 +180,14 @@ class solver_path:
         import torch
         with torch.cuda.device(self._device):
             check(lib().srbd_set_solver_path(self._prev), "srbd_set_solver_path")
+
+
+def build_id() -> str:
+    """Source hash the loaded libsrbd_mpc.so was built from (build.py source_hash)."""
+    try:
+        return lib().srbd_build_id().decode()
+    except NativeLibraryMissing:
+        return "unknown"
 
 
 def last_error() -> str:

@@ -185,6 +185,10 @@ class MPCControllerHIP(BaseMPCController):
         self.foot_wrench = torch.empty((B, 2, 6), dtype=torch.float32, device=dev)
         self.cost = torch.zeros(B, device=dev)
         self.tau = None  # (B, 2, ndof) float32, allocated by run_with_torque
+        # per-env status word of the last step (include/srbd_mpc.h SRBD_STATUS_*: 1 non-finite
+        # solution, 2 step length at its floor in the last iteration): set to an int32 (B,) tensor
+        # on the device to have run() fill it (None: not computed)
+        self.status = None
         return self
 
     def _prep_struct(self, keep: list, strict: bool = False) -> _native.MPCPrep:
@@ -258,11 +262,14 @@ class MPCControllerHIP(BaseMPCController):
                 if self.cfg.keep_solution else None)
         fin = (_native.ptr_array([t.data_ptr() for t in self.former_inputs])
                if self.cfg.keep_solution else None)
-        rc = _native.lib().srbd_mpc_step(
-            N, self.cfg.pdipm_iterations, B, float(self.cfg.y0), ctypes.byref(p), fin, outs,
-            self.foot_wrench.data_ptr(), 0 if J is None else J.shape[3], None if J is None else J.data_ptr(),
-            None if cb is None else cb.data_ptr(), None if J is None else self.tau.data_ptr(),
-            solver._stream_ptr())
+        args = (N, self.cfg.pdipm_iterations, B, float(self.cfg.y0), ctypes.byref(p), fin, outs,
+                self.foot_wrench.data_ptr(), 0 if J is None else J.shape[3], None if J is None else J.data_ptr(),
+                None if cb is None else cb.data_ptr(), None if J is None else self.tau.data_ptr())
+        if self.status is not None:
+            rc = _native.lib().srbd_mpc_step_ex(*args, solver._check_status(self.status, B, "MPCControllerHIP.status"),
+                                                solver._stream_ptr())
+        else:
+            rc = _native.lib().srbd_mpc_step(*args, solver._stream_ptr())
         _native.check(rc, "srbd_mpc_step")
         self.solution = self.buffers.outputs if self.cfg.keep_solution else None
 

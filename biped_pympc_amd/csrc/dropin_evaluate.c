@@ -9,6 +9,13 @@
 #ifndef SRBD_N
 #define SRBD_N 10
 #endif
+#ifndef SRBD_SHIM_ID
+#define SRBD_SHIM_ID "0000000000000000"
+#endif
+
+/* build provenance: hash of this shim, its configuration and libsrbd_mpc.so's build id
+ * (biped_pympc_amd/build.py _shim_hash), read from the file by build.py */
+__attribute__((used)) static const char srbd_shim_id_tag[] = "srbd-shim-id:" SRBD_SHIM_ID;
 
 float evaluate(const double* inputs[], double* work, double* outputs[], const int batch_size) {
 #if defined(SRBD_FN_FORMER)

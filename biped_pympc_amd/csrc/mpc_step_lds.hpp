@@ -105,7 +105,12 @@ __global__ __launch_bounds__(64) void mpc_step_lds_kernel(FusedArgs fa) {
   for (int e = lane; e < p; e += 64) C.Y[e] = fa.y0;
   __syncthreads();
   double res[4] = {0.0, 0.0, 0.0, 0.0};
-  C.newton(fa.n_iter, res);
+  bool floor_hit = false;
+  C.newton(fa.n_iter, res, floor_hit);
+  if (fa.status) {
+    const int st = C.status(res[3], floor_hit);
+    if (lane == 0) fa.status[env] = st;
+  }
   // ---- outputs (each optional) ----
   if (double* xo = fa.out[0])
     for (int e = lane; e < nz; e += 64) xo[(size_t)env * nz + e] = C.X[e];

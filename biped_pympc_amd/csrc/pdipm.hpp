@@ -45,7 +45,15 @@ struct SolverArgs {
   double* scratch;
   int* scratch_locks;
   int scratch_slots;
+  int* status;  // (batch) per-problem status word (kStatus* bits), or null: not written
 };
+
+// Per-problem status word (SURVEY.md 5 "failure detection"; the reference has only its clamps,
+// sparse_pdipm_solver.py:466-467,501-515): bit 0 a non-finite value in the returned x, s, z, y or
+// mu; bit 1 a combined-direction step length (primal or dual) at its 1e-12 floor in the last
+// iteration; bit 2 the QP was not stage-invariant and took the general solve (scratch fallback).
+constexpr int kStatusNonFinite = 1, kStatusStepFloor = 2, kStatusFallback = 4;
+__device__ __forceinline__ bool not_finite(double v) { return !__builtin_isfinite(v); }
 
 // iterative-refinement steps per direction in the LDS-resident and general kernels (the register
 // kernels' one step sits at the FP64 floor at N = 10 / 20)
@@ -626,7 +634,8 @@ struct SolverCtx {
 // a slot of the library's global scratch pool when a stage-invariant kernel meets a QP it cannot
 // take). `lane` >= 64 marks an idle lane (the second wave of a two-wave QP): it takes part in every
 // barrier and stores nothing.
-__device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in) {
+__device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in,
+                                                 int status_bits = 0) {
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;
@@ -679,6 +688,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   __syncthreads();
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
+  bool floor_hit = false;
   for (int it = 0; it < args.n_iter; ++it) {
     const double mu = C.residuals();
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
@@ -712,6 +722,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     C.solve();
     C.refine();
     const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
+    floor_hit = apc <= 1e-12 || adc <= 1e-12;  // the last iteration's value is reported
     __syncthreads();
     double szn = 0.0;
     for (int e = lane; e < nz; e += 64) C.X[e] = C.X[e] + apc * C.TV[e];
@@ -742,6 +753,15 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     ro[3] = mu_new;
     mo[0] = mu_new;
   }
+  if (args.status) {
+    bool nf = lane == 0 && not_finite(mu_new);
+    for (int e = lane; e < nz; e += 64) nf = nf || not_finite(C.X[e]);
+    for (int e = lane; e < m; e += 64) nf = nf || not_finite(C.S[e]) || not_finite(C.Z[e]);
+    for (int e = lane; e < p; e += 64) nf = nf || not_finite(C.Y[e]);
+    nf = __any(nf);
+    if (lane == 0)
+      args.status[env] = status_bits | (nf ? kStatusNonFinite : 0) | (floor_hit ? kStatusStepFloor : 0);
+  }
 }
 
 // A QP the stage-invariant kernels cannot take (not stage-invariant: any CCS input other than
@@ -759,8 +779,11 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
 __device__ __forceinline__ const SolverArgs& kernel_args() {
   return *(const SolverArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // constant -> generic address space
 }
+// `xchg`: an LDS int of the calling workgroup through which a multi-wave QP's waves agree on the slot
+// (wave 0 takes it; the other waves run the solve as idle lanes but read the slot's memory, so they
+// must see the same one); null for a one-wave QP.
 template <int kTag>
-__device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs& args, int env) {
+__device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs& args, int env, int* xchg) {
   const int n = args.scratch_slots;
   int slot = env % n;
   if (threadIdx.x == 0) {
@@ -768,11 +791,17 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
       slot = slot + 1 == n ? 0 : slot + 1;
       __builtin_amdgcn_s_sleep(8);
     }
+    if (xchg) *xchg = slot;
   }
-  slot = __shfl(slot, 0, 64);  // wave 0's slot (an idle second wave never touches the slot)
+  if (xchg) {
+    __syncthreads();
+    slot = *xchg;
+  } else {
+    slot = __shfl(slot, 0, 64);
+  }
   __threadfence();
   const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
-  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane);
+  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane, kStatusFallback);
   __syncthreads();
   __threadfence();
   if (threadIdx.x == 0) atomicExch(&args.scratch_locks[slot], 0);

@@ -768,7 +768,8 @@ struct FastCtx {
 
   // n_iter Mehrotra iterations from the iterate in X, S, Z, Y (sparse_pdipm_solver.py:376-521);
   // res = the last iteration's pre-update residual norms [|rx|, |rs|, |re|] and mu_new (:523-530)
-  __device__ void newton(int n_iter, double (&res)[4]) {
+  // floor_hit: a combined step length at its 1e-12 floor in the last iteration (status bit 1)
+  __device__ void newton(int n_iter, double (&res)[4], bool& floor_hit) {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
     double mu_new = 0.0;
     for (int it = 0; it < n_iter; ++it) {
@@ -802,6 +803,7 @@ struct FastCtx {
       solve(1, sigma * mu * 1.0);
       refine();
       const double apc = step_length(S, DS), adc = step_length(Z, DZ);
+      floor_hit = apc <= 1e-12 || adc <= 1e-12;
       __syncthreads();
       double szn = 0.0;
       for (int e = lane; e < nz; e += 64) X[e] = X[e] + apc * TV[e];
@@ -818,6 +820,16 @@ struct FastCtx {
       PROF_ADD(5);
     }
     res[3] = mu_new;
+  }
+
+  // status word of the returned iterate (pdipm.hpp kStatus*), for lane 0
+  __device__ int status(double mu_new, bool floor_hit) const {
+    const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
+    bool nf = lane == 0 && not_finite(mu_new);
+    for (int e = lane; e < nz; e += 64) nf = nf || not_finite(X[e]);
+    for (int e = lane; e < m; e += 64) nf = nf || not_finite(S[e]) || not_finite(Z[e]);
+    for (int e = lane; e < p; e += 64) nf = nf || not_finite(Y[e]);
+    return (__any(nf) ? kStatusNonFinite : 0) | (floor_hit ? kStatusStepFloor : 0);
   }
 
   __device__ double step_length(const double* v, const double* dv) const {
@@ -883,7 +895,7 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < 12 * N ? 0 : 12 * N) + e % 12]);
   const bool any_bad = __any(bad);
   if (any_bad) {
-    pdipm_general_scratch<100 + NT>(kernel_args(), env);  // the kernel's sole argument
+    pdipm_general_scratch<100 + NT>(kernel_args(), env, nullptr);  // the kernel's sole argument
     return;
   }
   // ---- per-QP constants ----
@@ -911,8 +923,9 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   __syncthreads();
 
   double res[4] = {0.0, 0.0, 0.0, 0.0};
+  bool floor_hit = false;
   PROF_MARK_CTX(C);
-  C.newton(args.n_iter, res);
+  C.newton(args.n_iter, res, floor_hit);
   PROF_FLUSH(C);
   double* xo = solver_out(args, 0) + (size_t)env * nz;
   double* so = solver_out(args, 1) + (size_t)env * m;
@@ -927,6 +940,10 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) ro[k] = res[k];
     mo[0] = res[3];
+  }
+  if (args.status) {
+    const int st = C.status(res[3], floor_hit);
+    if (lane == 0) args.status[env] = st;
   }
 }
 

@@ -357,7 +357,11 @@ __device__ __forceinline__ double grow4(const double* gf, int k, const double* x
   return g[o] * xu[foot_colj(f, o)] + g[2] * xu[foot_colj(f, 2)];
 }
 
-template <int N>
+// kFReg: every entry of f and b this lane uses held in registers (the fused kernel, which computes
+// them); false: f's slots t >= 1 and b's x-moment slot are re-read from memory (L2) each iteration --
+// the CCS kernel, whose stage-invariance check and three iterate initialisations leave no room for
+// them: held, they spilled 4 VGPRs (scratch reloads in the Newton loop)
+template <int N, bool kFReg = true>
 struct RegCtx {
   static constexpr int TPB = reg_tpb(N);
   using Lo = RegLayout<N>;
@@ -407,13 +411,13 @@ struct RegCtx {
   double fxr[SX], fur[SX], bvr[SE], hvr[SI];
   __device__ void load_qp_vectors() {
 #pragma unroll
-    for (int t = 0; t < SX; ++t) {
+    for (int t = 0; t < (kFReg ? SX : 1); ++t) {
       const int c = min(lane + TPB * t, nx - 1);
       fxr[t] = fg[c];
       fur[t] = fg[nx + c];
     }
 #pragma unroll
-    for (int t = 0; t < SE; ++t) {
+    for (int t = 0; t < (kFReg ? SE : 2); ++t) {
       const ERow q = erow(lane, t);
       bvr[t] = bg[q.valid ? q.e : 0];
     }
@@ -507,7 +511,7 @@ struct RegCtx {
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
         const int k = div12(c) + 1, j = c - m24(k - 1, 12);
-        const double v = Hu[12 + j] * X[c] + fx[t];
+        const double v = Hu[12 + j] * X[c] + ((kFReg || t == 0) ? fx[t] : fg[c]);
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
         ay = fma(k < N ? 1.0 : 0.0, my, ay);
@@ -519,7 +523,7 @@ struct RegCtx {
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
         const int i = div12(c), j = c - m24(i, 12);
-        const double v = Hu[j] * X[nx + c] + fu[t];
+        const double v = Hu[j] * X[nx + c] + ((kFReg || t == 0) ? fu[t] : fg[nx + c]);
         // G^T z on the foot columns and the x-moment terms on columns 6 / 9, formed in every lane
         // (clamped foot index) and selected
         const int fj = foot_of(j), f = fj >= 0 ? fj : 0;
@@ -545,7 +549,7 @@ struct RegCtx {
       const ERow q = erow(lane, 2);
       if (q.valid) {
         const int w = q.r;
-        re[2] = SG[6 + w] * X[nx + 12 * q.i + (w ? 9 : 6)] - bv[2];
+        re[2] = SG[6 + w] * X[nx + 12 * q.i + (w ? 9 : 6)] - (kFReg ? bv[2] : bg[q.e]);
         REm[q.e - nx] = re[2];
       }
     }
@@ -1243,6 +1247,7 @@ struct FusedArgs {
   const float *jac, *contact;  // (B, 2, 6, ndof), (B, 2) float32 for tau
   float* tau;      // (B, 2, ndof) float32, or null
   int ndof;
+  int* status;     // (B) per-problem status word (pdipm.hpp kStatus*), or null
 };
 
 // Body shared by the solver kernel (kFused = false: the QP comes from qp_former's CCS outputs and is
@@ -1260,7 +1265,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   if (env >= (kFused ? fa.batch : args.batch)) return;
   const int lane = threadIdx.x;
   constexpr int nz = Lo::nz, m = Lo::m, p = Lo::p, nx = Lo::nx, SI = Lo::SI;
-  RegCtx<N> C;
+  RegCtx<N, kFused> C;
   C.L = smem;
   C.lane = lane;
   double *Mc = smem + Lo::Mc, *Cc = smem + Lo::Cc, *Nd = smem + Lo::Nd, *Gf = smem + Lo::Gf,
@@ -1434,7 +1439,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       qp_sync<TPB>();  // RED is reused by the first block reduction
     }
     if (bad) {  // not stage-invariant: the general solve, in this launch (pdipm_general_scratch)
-      pdipm_general_scratch<N>(kernel_args(), env);  // the kernel's sole argument
+      // the kernel's sole argument; a multi-wave QP's waves agree on the slot through the DMY sink
+      pdipm_general_scratch<N>(kernel_args(), env, TPB > 64 ? reinterpret_cast<int*>(smem + Lo::DMY) : nullptr);
       return;
     }
   }
@@ -1617,6 +1623,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.template solve_finish<true>();
     double apc, adc;
     C.step_lengths(apc, adc);
+    // status bit 1 (a step length at its 1e-12 floor in the last iteration), kept in LDS: SG[15] is
+    // unused (SG[0..9] are the x-moment constants) and a register held across the loop would spill
+    if (it == n_iter - 1 && lane == 0) SG[15] = (apc <= 1e-12 || adc <= 1e-12) ? 1.0 : 0.0;
     qp_sync<TPB>();
     double szn = 0.0;
     ul = C.fresh_lane();
@@ -1679,6 +1688,17 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       ro[3] = mu_new;
     }
     if (double* mo = outp(5)) mo[env] = mu_new;
+  }
+  if (int* st = kFused ? fa.status : args.status) {  // uniform: every wave takes part in the vote
+    const int ul = C.fresh_lane();
+    bool nf = ul == 0 && not_finite(mu_new);
+    for (int e = ul; e < nz; e += TPB) nf = nf || not_finite(X[e]);
+    for (int e = ul; e < p; e += TPB) nf = nf || not_finite(Y[e]);
+#pragma unroll
+    for (int t = 0; t < SI; ++t)
+      if (RegCtx<N>::full_slot(t, m) || ul + TPB * t < m) nf = nf || not_finite(C.s[t]) || not_finite(C.z[t]);
+    nf = C.block_any(nf);
+    if (lane == 0) st[env] = (nf ? kStatusNonFinite : 0) | (SG[15] != 0.0 ? kStatusStepFloor : 0);
   }
   if constexpr (kFused) {
     if (fa.wrench) {  // u0 -> foot wrench (+ stance torque): srbd_u0_wrench_torque's arithmetic

@@ -22,7 +22,14 @@
 #include "regN.hpp"
 #include "device_state.hpp"
 
+#ifndef SRBD_BUILD_ID
+#define SRBD_BUILD_ID "0000000000000000"  // diagnostic builds outside biped_pympc_amd/build.py
+#endif
+
 namespace {
+
+// "srbd-build-id:" + the 16-hex source hash (build.py source_hash); build.py reads it from the file
+__attribute__((used)) const char kBuildIdTag[] = "srbd-build-id:" SRBD_BUILD_ID;
 
 thread_local std::string g_last_error;
 
@@ -92,16 +99,24 @@ struct ScratchPool {
 srbd::PerDevice<ScratchPool> g_scratch;
 std::mutex g_scratch_mu;
 
-int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
+// the current device's pool, allocated on first use (`s`: the stream of the calling launch, checked for
+// capture; null from srbd_prepare_device)
+ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
+  rc = 0;
   const int dev = current_device();
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   ScratchPool* pool = g_scratch.at(dev);
-  if (!pool) return set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
+  if (!pool) {
+    rc = set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
+    return nullptr;
+  }
   if (!pool->buf) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
-      return set_error(kErrInvalid, "srbd solver: first call on this device inside a stream capture (the "
-                                    "scratch pool is allocated on first use: call once before capturing)");
+    if (check_capture && hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+      rc = set_error(kErrInvalid, "srbd solver: first call on this device inside a stream capture (the "
+                                  "scratch pool is allocated on first use: call srbd_prepare_device() first)");
+      return nullptr;
+    }
     const size_t per_slot = (size_t)srbd::SolverLayout(srbd::kMaxN).total;
     double* buf = nullptr;
     int* locks = nullptr;
@@ -112,11 +127,19 @@ int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
     if (e != hipSuccess) {
       (void)hipFree(buf);
       (void)hipFree(locks);
-      return set_error((int)e, "srbd solver: scratch pool allocation");
+      rc = set_error((int)e, "srbd solver: scratch pool allocation");
+      return nullptr;
     }
     pool->buf = buf;
     pool->locks = locks;
   }
+  return pool;
+}
+
+int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
+  int rc = 0;
+  ScratchPool* pool = scratch_pool(s, true, rc);
+  if (!pool) return rc;
   a.scratch = pool->buf;
   a.scratch_locks = pool->locks;
   a.scratch_slots = kScratchSlots;
@@ -213,6 +236,8 @@ extern "C" {
 
 int srbd_abi_version(void) { return SRBD_ABI_VERSION; }
 
+const char* srbd_build_id(void) { return kBuildIdTag + sizeof("srbd-build-id:") - 1; }
+
 const char* srbd_last_error(void) { return g_last_error.c_str(); }
 
 size_t srbd_solver_lds_bytes(int horizon) { return horizon_ok(horizon) ? solver_lds_bytes(horizon) : 0; }
@@ -227,6 +252,11 @@ int srbd_set_solver_path(int path) {
 }
 
 int srbd_get_solver_path(void) { return solver_path(); }
+
+int srbd_prepare_device(void) {
+  int rc = 0;
+  return scratch_pool(nullptr, false, rc) ? 0 : rc;
+}
 
 size_t srbd_mpc_workspace_doubles(int horizon, int batch) {
   if (!horizon_ok(horizon) || batch < 0) return 0;
@@ -286,7 +316,7 @@ int srbd_qp_former(int horizon, int batch, const double* const* inputs, double* 
 }
 
 static int pdipm_common(int horizon, int n_iter, int batch, double y0, int init_mode,
-                        const double* const* inputs, double* const* outputs, void* stream) {
+                        const double* const* inputs, double* const* outputs, int* status, void* stream) {
   if (!horizon_ok(horizon) || n_iter < 1 || batch < 0 || !inputs || !outputs)
     return set_error(kErrInvalid, "srbd_pdipm: bad arguments");
   if (batch == 0) return 0;
@@ -305,27 +335,36 @@ static int pdipm_common(int horizon, int n_iter, int batch, double y0, int init_
   a.batch = batch;
   a.init_mode = init_mode;
   a.y0 = y0;
+  a.status = status;
   return launch_solver(a, (hipStream_t)stream);
 }
 
 int srbd_pdipm(int horizon, int n_iter, int batch, const double* const* inputs,
                double* const* outputs, void* stream) {
-  return pdipm_common(horizon, n_iter, batch, 0.0, 0, inputs, outputs, stream);
+  return pdipm_common(horizon, n_iter, batch, 0.0, 0, inputs, outputs, nullptr, stream);
 }
 
 int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double* const* inputs,
                     double* const* outputs, void* stream) {
-  return pdipm_common(horizon, n_iter, batch, y0, 1, inputs, outputs, stream);
+  return pdipm_common(horizon, n_iter, batch, y0, 1, inputs, outputs, nullptr, stream);
 }
 
 int srbd_pdipm_ccs(int horizon, int n_iter, int batch, const double* const* inputs, double* const* outputs,
                    void* stream) {
   if (!inputs || (batch > 0 && !inputs[6])) return set_error(kErrInvalid, "srbd_pdipm_ccs: null x_init");
-  return pdipm_common(horizon, n_iter, batch, 0.0, 2, inputs, outputs, stream);
+  return pdipm_common(horizon, n_iter, batch, 0.0, 2, inputs, outputs, nullptr, stream);
 }
 
-int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
-                   double* qp_workspace, double* const* outputs, void* stream) {
+int srbd_pdipm_ex(int horizon, int n_iter, int batch, int init_mode, double y0, const double* const* inputs,
+                  double* const* outputs, int* status, void* stream) {
+  if (init_mode < 0 || init_mode > 2) return set_error(kErrInvalid, "srbd_pdipm_ex: init_mode 0, 1 or 2");
+  if (init_mode == 2 && (!inputs || (batch > 0 && !inputs[6])))
+    return set_error(kErrInvalid, "srbd_pdipm_ex: null x_init");
+  return pdipm_common(horizon, n_iter, batch, init_mode == 1 ? y0 : 0.0, init_mode, inputs, outputs, status, stream);
+}
+
+static int mpc_solve_two_kernels(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                                 double* qp_workspace, double* const* outputs, int* status, void* stream) {
   if (!horizon_ok(horizon) || !qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve: bad arguments");
   const size_t N = (size_t)horizon, B = (size_t)(batch < 0 ? 0 : batch);
   double* H = qp_workspace;
@@ -337,7 +376,12 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
   double* qp[6] = {H, f, A, b, G, d};
   if (int rc = srbd_qp_former(horizon, batch, former_inputs, qp, stream)) return rc;
   const double* sin[10] = {H, G, A, f, d, b, nullptr, nullptr, nullptr, nullptr};
-  return srbd_pdipm_cold(horizon, n_iter, batch, y0, sin, outputs, stream);
+  return pdipm_common(horizon, n_iter, batch, y0, 1, sin, outputs, status, stream);
+}
+
+int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                   double* qp_workspace, double* const* outputs, void* stream) {
+  return mpc_solve_two_kernels(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, nullptr, stream);
 }
 
 // launch of the fused / controller-step kernel (a fully set up FusedArgs): the register kernels at
@@ -365,12 +409,12 @@ static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
   return e == hipSuccess ? 0 : set_error((int)e, "mpc_step_reg_kernel launch");
 }
 
-int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
-                         double* qp_workspace, double* const* outputs, void* stream) {
+int srbd_mpc_solve_fused_ex(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                            double* qp_workspace, double* const* outputs, int* status, void* stream) {
   if (!horizon_ok(horizon)) return set_error(kErrInvalid, "srbd_mpc_solve_fused: bad horizon");
   if (solver_path() != 0) {  // a non-auto solver path: former + that solver kernel
     if (!qp_workspace) return set_error(kErrInvalid, "srbd_mpc_solve_fused: a non-auto solver path needs qp_workspace");
-    return srbd_mpc_solve(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, stream);
+    return mpc_solve_two_kernels(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, status, stream);
   }
   if (n_iter < 1 || batch < 0 || !former_inputs || !outputs)
     return set_error(kErrInvalid, "srbd_mpc_solve_fused: bad arguments");
@@ -391,7 +435,13 @@ int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const do
   a.n_iter = n_iter;
   a.batch = batch;
   a.y0 = y0;
+  a.status = status;
   return launch_step(a, (hipStream_t)stream);
+}
+
+int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                         double* qp_workspace, double* const* outputs, void* stream) {
+  return srbd_mpc_solve_fused_ex(horizon, n_iter, batch, y0, former_inputs, qp_workspace, outputs, nullptr, stream);
 }
 
 // srbd_mpc_prep (host struct of device pointers + constants) -> the kernels' PrepArgs
@@ -435,9 +485,10 @@ static int fill_prep(const srbd_mpc_prep* p, srbd::PrepArgs& a, const char* who)
   return 0;
 }
 
-int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
-                  double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
-                  const float* contact_jacobian, const float* contact_bool, float* tau, void* stream) {
+int srbd_mpc_step_ex(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
+                     double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
+                     const float* contact_jacobian, const float* contact_bool, float* tau, int* status,
+                     void* stream) {
   if (!horizon_ok(horizon)) return set_error(kErrInvalid, "srbd_mpc_step: bad horizon");
   if (n_iter < 1 || batch < 0 || !prep || (tau && (ndof < 1 || ndof > 64)))
     return set_error(kErrInvalid, "srbd_mpc_step: bad arguments");
@@ -465,7 +516,15 @@ int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_
   a.n_iter = n_iter;
   a.batch = batch;
   a.y0 = y0;
+  a.status = status;
   return launch_step(a, (hipStream_t)stream);
+}
+
+int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
+                  double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
+                  const float* contact_jacobian, const float* contact_bool, float* tau, void* stream) {
+  return srbd_mpc_step_ex(horizon, n_iter, batch, y0, prep, former_inputs, outputs, foot_wrench, ndof,
+                          contact_jacobian, contact_bool, tau, nullptr, stream);
 }
 
 int srbd_pattern_ccs(int horizon, int which, int* colptr, int* rowind) {

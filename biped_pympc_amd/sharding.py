@@ -37,8 +37,11 @@ class ShardedMPC:
     def __init__(self, N: int, n_iter: int, total_envs: int, device=None, y0: float = 1.0,
                  group=None, solve_fn: Callable[[Sequence[torch.Tensor]], torch.Tensor] | None = None):
         self.N, self.n_iter, self.total, self.y0, self.group = N, n_iter, total_envs, y0, group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # with a process group the gather always runs through it, even at world size 1 (a one-GPU
+        # job launched under torch.distributed exercises the same RCCL path as an 8-GPU one)
+        self.collective = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.collective else 1
+        self.rank = dist.get_rank(group) if self.collective else 0
         self.lo, self.hi = shard_bounds(total_envs, self.world, self.rank)
         self.sizes = [shard_bounds(total_envs, self.world, r) for r in range(self.world)]
         self.slot = max(h - l for l, h in self.sizes)  # padded per-rank block of the gather
@@ -91,7 +94,7 @@ class ShardedMPC:
             raise ValueError(f"rank {self.rank}: expected {self.local_envs} envs, got {local_inputs[0].shape[0]}")
         self.x_local = self._solve(local_inputs)
         u0 = self.x_local[:, 12 * self.N:12 * self.N + 12]
-        if self.world == 1:  # the next solve reuses x_local: hand out a copy (96 B/env)
+        if not self.collective:  # the next solve reuses x_local: hand out a copy (96 B/env)
             return PendingGather(u0.clone(), None, None)
         if self._abuf is None:
             mk = lambda *sh: torch.zeros(sh, dtype=torch.float64, device=self.device)  # noqa: E731
@@ -118,8 +121,8 @@ class ShardedMPC:
 
     def gather_u0(self, u0_local: torch.Tensor) -> torch.Tensor:
         """All-gather the shards' u0 into ``self.u0_all`` in global env order."""
-        if self.world == 1:
-            self.u0_all = u0_local  # single GPU: a view of the solution, no copy in the step
+        if not self.collective:
+            self.u0_all = u0_local  # no process group: a view of the solution, no copy in the step
             return self.u0_all
         into_tensor = dist.get_backend(self.group) == "nccl"  # RCCL; gloo lacks the fused form
         if not self._ragged:

@@ -49,17 +49,30 @@ def qp_former(inputs: list[torch.Tensor], N: int, outputs: list[torch.Tensor] | 
     return outputs
 
 
+def _check_status(status, B: int, what: str):
+    """status: None, or an int32 (B,) CUDA tensor on the current device for the per-problem status
+    word (include/srbd_mpc.h SRBD_STATUS_*: 1 non-finite result, 2 step length at its floor in the
+    last iteration, 4 general fallback taken)."""
+    if status is None:
+        return None
+    if (not status.is_cuda or status.dtype != torch.int32 or status.numel() != B or not status.is_contiguous()
+            or status.device.index != torch.cuda.current_device()):
+        raise ValueError(f"{what}: status must be a contiguous int32 CUDA tensor of {B} elements on the current device")
+    return status.data_ptr()
+
+
 def _alloc_solver_outputs(B: int, N: int, device) -> list[torch.Tensor]:
     return [torch.empty((B, w), dtype=torch.float64, device=device) for w in Dims(N).solver_out_nnz]
 
 
 def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_iter: int,
-          y0: float = 1.0, outputs: list[torch.Tensor] | None = None):
+          y0: float = 1.0, outputs: list[torch.Tensor] | None = None, status: torch.Tensor | None = None):
     """Sparse PDIPM, n_iter Mehrotra iterations (sparse_pdipm_solver.py:357-534).
 
     qp: [Q_val, G_val, A_val, f, h, b]; iterate: [x, s, z, y] or None for the GPU caller's cold
     start (x=0, s=max(h,1), z=1, y=y0; mpc_controller_cusadi.py:138-141).
-    Returns [x, s, z, y, residuals(4), mu(1)].
+    Returns [x, s, z, y, residuals(4), mu(1)]; ``status`` (int32 (B,), optional) receives the
+    per-problem status word.
     """
     d = Dims(N)
     B = qp[0].shape[0]
@@ -71,7 +84,10 @@ def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_
     L = _native.lib()
     ptrs = _native.ptr_array([t.data_ptr() if t is not None else 0 for t in ins])
     outp = _native.ptr_array([t.data_ptr() for t in outputs])
-    if iterate is None:
+    st = _check_status(status, B, "pdipm")
+    if st is not None:
+        rc = L.srbd_pdipm_ex(N, n_iter, B, 1 if iterate is None else 0, float(y0), ptrs, outp, st, _stream_ptr())
+    elif iterate is None:
         rc = L.srbd_pdipm_cold(N, n_iter, B, float(y0), ptrs, outp, _stream_ptr())
     else:
         rc = L.srbd_pdipm(N, n_iter, B, ptrs, outp, _stream_ptr())
@@ -80,7 +96,7 @@ def pdipm(qp: list[torch.Tensor], iterate: list[torch.Tensor] | None, N: int, n_
 
 
 def pdipm_ccs(qp: list[torch.Tensor], x_init: torch.Tensor, N: int, n_iter: int,
-              outputs: list[torch.Tensor] | None = None):
+              outputs: list[torch.Tensor] | None = None, status: torch.Tensor | None = None):
     """The reference's ``_ccs`` solver (sparse_pdipm_solver_ccs, sparse_pdipm_solver.py:4-35): n_iter
     Mehrotra iterations from x = x_init, s = max(h - G x_init, 1), z = 1, y = 0
     (initialize_pdipm_variables, :537-558). qp: [Q_val, G_val, A_val, f, h, b]; x_init (B, 24N).
@@ -92,9 +108,13 @@ def pdipm_ccs(qp: list[torch.Tensor], x_init: torch.Tensor, N: int, n_iter: int,
     if outputs is None:
         outputs = _alloc_solver_outputs(B, N, qp[0].device)
     _check_batch(outputs, d.solver_out_nnz, B, "pdipm_ccs outputs")
-    rc = _native.lib().srbd_pdipm_ccs(N, n_iter, B, _native.ptr_array([t.data_ptr() if t is not None else 0
-                                                                       for t in ins]),
-                                      _native.ptr_array([t.data_ptr() for t in outputs]), _stream_ptr())
+    ptrs = _native.ptr_array([t.data_ptr() if t is not None else 0 for t in ins])
+    outp = _native.ptr_array([t.data_ptr() for t in outputs])
+    st = _check_status(status, B, "pdipm_ccs")
+    if st is not None:
+        rc = _native.lib().srbd_pdipm_ex(N, n_iter, B, 2, 0.0, ptrs, outp, st, _stream_ptr())
+    else:
+        rc = _native.lib().srbd_pdipm_ccs(N, n_iter, B, ptrs, outp, _stream_ptr())
     _native.check(rc, "srbd_pdipm_ccs")
     return outputs
 
@@ -124,7 +144,8 @@ class MPCSolveBuffers:
 
 
 def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float = 1.0,
-              buffers: MPCSolveBuffers | None = None, fused: bool = True, keep_qp: bool = False):
+              buffers: MPCSolveBuffers | None = None, fused: bool = True, keep_qp: bool = False,
+              status: torch.Tensor | None = None):
     """qp_former + cold-started PDIPM in one stream with no host synchronisation.
 
     Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
@@ -133,7 +154,8 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     (``srbd_mpc_solve_fused``; the register kernels at N = 10 and 20, the LDS-resident step kernel at
     other horizons): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to their
     ``buffers.workspace`` slots); ``False`` runs the former and the solver as two kernels with the
-    full QP in the workspace. Both give the same bits.
+    full QP in the workspace. Both give the same bits. ``status`` (int32 (B,), optional) receives
+    the per-problem status word.
     """
     d = Dims(N)
     B = former_inputs[0].shape[0]
@@ -147,9 +169,15 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     # the fused kernel runs under the auto solver path (any horizon); otherwise the former writes the
     # whole QP into the workspace for the solver kernel
     one_kernel = fused and _native.current_solver_path() == 0
-    rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(N, n_iter, B, float(y0),
-                          _native.ptr_array([t.data_ptr() for t in former_inputs]),
-                          buffers.workspace.data_ptr() if (keep_qp or not one_kernel) else None,
-                          _native.ptr_array([t.data_ptr() for t in buffers.outputs]), _stream_ptr())
+    args = (N, n_iter, B, float(y0), _native.ptr_array([t.data_ptr() for t in former_inputs]),
+            buffers.workspace.data_ptr() if (keep_qp or not one_kernel) else None,
+            _native.ptr_array([t.data_ptr() for t in buffers.outputs]))
+    st = _check_status(status, B, "mpc_solve")
+    if st is not None:  # the two-kernel form runs under srbd_mpc_solve_fused_ex's non-auto branch alike
+        if not fused and one_kernel:
+            raise ValueError("mpc_solve: status with fused=False needs a non-auto solver path")
+        rc = L.srbd_mpc_solve_fused_ex(*args, st, _stream_ptr())
+    else:
+        rc = (L.srbd_mpc_solve_fused if fused else L.srbd_mpc_solve)(*args, _stream_ptr())
     _native.check(rc, "srbd_mpc_solve")
     return buffers.outputs

@@ -39,6 +39,9 @@ float evaluate(const double* inputs[], double* work, double* outputs[], const in
 /* ---- Extended API (libsrbd_mpc.so) ------------------------------------------------------------ */
 int srbd_abi_version(void);
 const char* srbd_last_error(void);
+/* Build provenance: 16 hex digits of sha256 over the library's sources and compile flags
+ * (biped_pympc_amd/build.py source_hash); smoke() and bench.py print it. */
+const char* srbd_build_id(void);
 
 /* CusADi-ABI implementations with explicit configuration (what the thin libraries call). */
 float srbd_evaluate_qp_former(int horizon, const double* inputs[], double* work, double* outputs[],
@@ -73,6 +76,21 @@ int srbd_pdipm_cold(int horizon, int n_iter, int batch, double y0, const double*
 int srbd_pdipm_ccs(int horizon, int n_iter, int batch, const double* const* inputs, double* const* outputs,
                    void* stream);
 
+/* Per-problem status word (failure detection; the reference has no such output, only its
+ * clamps, sparse_pdipm_solver.py:466-467,501-515): int32 per env, OR of
+ *   SRBD_STATUS_NONFINITE  a NaN / Inf in the returned x, s, z, y or mu
+ *   SRBD_STATUS_STEP_FLOOR a combined-direction step length (primal or dual) at its 1e-12 floor in the
+ *                          last iteration (the iterate is stalled at the boundary)
+ *   SRBD_STATUS_FALLBACK   the QP was not stage-invariant and took the general solve
+ * Written by the *_ex entry points when status != NULL (device memory, batch ints). */
+#define SRBD_STATUS_NONFINITE 1
+#define SRBD_STATUS_STEP_FLOOR 2
+#define SRBD_STATUS_FALLBACK 4
+
+/* srbd_pdipm (init_mode 0), srbd_pdipm_cold (1, y = y0) or srbd_pdipm_ccs (2) with the status word. */
+int srbd_pdipm_ex(int horizon, int n_iter, int batch, int init_mode, double y0, const double* const* inputs,
+                  double* const* outputs, int* status, void* stream);
+
 /* Whole MPC QP step: qp_former -> cold-start PDIPM (n_iter iterations), one stream, no host sync.
  * `qp_workspace` is caller-owned device memory of srbd_mpc_workspace_doubles(horizon, batch)
  * doubles that receives H, f, A, b, G, d (CCS, batched). outputs as srbd_pdipm. */
@@ -88,6 +106,9 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
  * not written). */
 int srbd_mpc_solve_fused(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
                          double* qp_workspace, double* const* outputs, void* stream);
+/* srbd_mpc_solve_fused with the status word (status may be NULL). */
+int srbd_mpc_solve_fused_ex(int horizon, int n_iter, int batch, double y0, const double* const* former_inputs,
+                            double* qp_workspace, double* const* outputs, int* status, void* stream);
 
 /* LDS bytes one solver workgroup (one QP) uses at this horizon (0 if unsupported). */
 size_t srbd_solver_lds_bytes(int horizon);
@@ -105,9 +126,19 @@ size_t srbd_solver_lds_bytes(int horizon);
  * solver path -- is kept per device (csrc/device_state.hpp). */
 int srbd_set_solver_path(int path);
 /* The solver path in effect for the current HIP device (0 if never set). srbd_mpc_solve_fused under a
- * non-auto path runs srbd_mpc_solve and so needs qp_workspace; srbd_mpc_step always runs the fused
- * register kernel (its QPs are stage-invariant by construction) and ignores the path. */
+ * non-auto path runs srbd_mpc_solve and so needs qp_workspace; srbd_mpc_step ignores the path and
+ * always runs its one-launch step kernel (its QPs are stage-invariant by construction): the
+ * register-resident kernel at N = 2..32, the LDS-resident step kernel at N = 1. */
 int srbd_get_solver_path(void);
+
+/* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the
+ * stage-invariant kernels (256 slots, ~39 MB of HBM, plus their lock words) -- on the current HIP
+ * device, synchronising it. Optional: the first srbd_pdipm* / srbd_mpc_solve* / evaluate call on a
+ * device does the same, but that first call must then not be made inside a stream capture (it returns
+ * an error there): call this, or make one ordinary call, before capturing a graph. Returns 0 or an
+ * error code. (The pool's lock words are released by the workgroups that take them; a kernel that
+ * faults leaves the HIP context unusable anyway.) */
+int srbd_prepare_device(void);
 
 /* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
  * offset maps the kernels use to address A_val/G_val. colptr has 24*horizon+1 entries, rowind nnz.
@@ -173,6 +204,11 @@ int srbd_prepare_inputs(int horizon, int batch, const srbd_mpc_prep* prep, doubl
 int srbd_mpc_step(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
                   double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
                   const float* contact_jacobian, const float* contact_bool, float* tau, void* stream);
+/* srbd_mpc_step with the status word (status may be NULL). */
+int srbd_mpc_step_ex(int horizon, int n_iter, int batch, double y0, const srbd_mpc_prep* prep,
+                     double* const* former_inputs, double* const* outputs, float* foot_wrench, int ndof,
+                     const float* contact_jacobian, const float* contact_bool, float* tau, int* status,
+                     void* stream);
 
 /* u0 = x[:, 12N:12N+12] -> foot wrench (B,2,6) float32 in the body frame, x-moments zeroed and
  * negated as mpc_controller_cusadi.py:186-203. rotation_body (B,3,3) float32 row-major. */

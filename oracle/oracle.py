@@ -83,8 +83,14 @@ def qp_former(N: int, inputs, B: int | None = None, nthreads: int = 0):
     return [o[0] for o in outs] if single else outs
 
 
-def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0):
-    """inputs: Q_val, G_val, A_val, f, h, b, x, s, z, y as (B, nnz). Returns x, s, z, y, res(4), mu(1)."""
+def _status_arg(status):
+    return None if status is None else status.ctypes.data_as(_I32P)
+
+
+def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0, status: np.ndarray | None = None):
+    """inputs: Q_val, G_val, A_val, f, h, b, x, s, z, y as (B, nnz). Returns x, s, z, y, res(4), mu(1).
+    status: an int32 (B,) array receiving the per-problem status word (srbd_oracle.c); with it a
+    failed factorisation is reported there instead of raising."""
     register(N)
     d = layout.Dims(N)
     single = np.asarray(inputs[0]).ndim == 1
@@ -93,7 +99,7 @@ def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0):
     ins = [_as_batch(a, w, B) for a, w in zip(inputs, d.solver_in_nnz)]
     outs = [np.zeros((B, w)) for w in d.solver_out_nnz]
     rc = lib().oracle_pdipm_batch(ctypes.c_int(N), ctypes.c_int(n_iter), ctypes.c_int(B),
-                                  _ptr_array(ins), _ptr_array(outs), ctypes.c_int(nthreads))
+                                  _ptr_array(ins), _ptr_array(outs), ctypes.c_int(nthreads), _status_arg(status))
     if rc < 0:
         raise RuntimeError("oracle_pdipm_batch failed")
     if rc > 0:
@@ -102,8 +108,8 @@ def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0):
 
 
 def mpc_solve(N: int, n_iter: int, former_inputs, y0: float = 1.0, B: int | None = None,
-              nthreads: int = 0):
-    """Former + GPU-caller init (x=0, s=max(d,1), z=1, y=y0) + n_iter iterations."""
+              nthreads: int = 0, status: np.ndarray | None = None):
+    """Former + GPU-caller init (x=0, s=max(d,1), z=1, y=y0) + n_iter iterations (status: as pdipm)."""
     register(N)
     d = layout.Dims(N)
     if B is None:
@@ -112,7 +118,7 @@ def mpc_solve(N: int, n_iter: int, former_inputs, y0: float = 1.0, B: int | None
     outs = [np.zeros((B, w)) for w in d.solver_out_nnz]
     rc = lib().oracle_mpc_solve_batch(ctypes.c_int(N), ctypes.c_int(n_iter), ctypes.c_double(y0),
                                       ctypes.c_int(B), _ptr_array(ins), _ptr_array(outs),
-                                      ctypes.c_int(nthreads))
+                                      ctypes.c_int(nthreads), _status_arg(status))
     if rc < 0:
         raise RuntimeError("oracle_mpc_solve_batch failed")
     if rc > 0:

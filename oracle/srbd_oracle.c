@@ -545,9 +545,21 @@ static double step_length(int m, const double *v, const double *dv) {
   return fmax(fmin(1.0, 0.99 * mn), 1e-12);
 }
 
+/* Per-problem status word (not a reference output; the build's failure-detection hook, SURVEY.md 5,
+ * computed here with the same definition as the HIP kernels so tests can compare them):
+ * bit 0 -- a non-finite value in the returned x, s, z, y or mu; bit 1 -- a combined-direction step
+ * length (primal or dual) at its 1e-12 floor (sparse_pdipm_solver.py:501-502) in the last iteration.
+ * (Bit 2, "solved by the general fallback", exists only on the GPU.) */
+static int nonfinite(const double *v, int n) {
+  for (int i = 0; i < n; ++i)
+    if (!isfinite(v[i])) return 1;
+  return 0;
+}
+
 /* sparse_pdipm_multiple_iterations, sparse_pdipm_solver.py:357-534.
- * in : Q_val, G_val, A_val, f, h, b, x, s, z, y        out: x, s, z, y, residuals(4), mu(1) */
-int oracle_pdipm(int N, int n_iter, const double *const in[10], double *const out[6]) {
+ * in : Q_val, G_val, A_val, f, h, b, x, s, z, y        out: x, s, z, y, residuals(4), mu(1)
+ * status: NULL, or the status word above. */
+int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const out[6], int *status) {
   if (N < 1 || N > MAXN || !g_pat[N].set || n_iter < 1) return -1;
   if (build_kkt_symbolic(N)) return -1;
   const pattern_t *P = &g_pat[N];
@@ -634,6 +646,8 @@ int oracle_pdipm(int N, int n_iter, const double *const in[10], double *const ou
     for (int k = 0; k < n; ++k) sc[k] = sa[k] + sc[k]; /* combined direction */
     const double *dx = sc, *ds = sc + nz, *dz = sc + nz + m, *dy = sc + nz + 2 * m;
     const double apc = step_length(m, s, ds), adc = step_length(m, z, dz);
+    const int floor_hit = apc <= 1e-12 || adc <= 1e-12;
+    if (status && it == n_iter - 1) *status = floor_hit ? 2 : 0;
     for (int k = 0; k < nz; ++k) x[k] = x[k] + apc * dx[k];
     for (int k = 0; k < m; ++k) s[k] = fmax(s[k] + apc * ds[k], 1e-8);
     for (int k = 0; k < m; ++k) z[k] = fmax(fmax(z[k] + adc * dz[k], 1e-8), 1e-8);
@@ -656,10 +670,16 @@ int oracle_pdipm(int N, int n_iter, const double *const in[10], double *const ou
   memcpy(out[3], y, sizeof(double) * p);
   memcpy(out[4], res, sizeof(double) * 4);
   out[5][0] = mu_new;
+  if (status && (nonfinite(x, nz) || nonfinite(s, m) || nonfinite(z, m) || nonfinite(y, p) || !isfinite(mu_new)))
+    *status |= 1;
   free(x); free(s); free(z); free(y);
   free(w.Kx); free(w.Lx); free(w.Li); free(w.D); free(w.Y); free(w.Lnz); free(w.Pattern); free(w.Flag);
   free(rx); free(rs); free(re); free(tmp); free(sa); free(sc); free(Gx); free(sinv);
   return rc;
+}
+
+int oracle_pdipm(int N, int n_iter, const double *const in[10], double *const out[6]) {
+  return oracle_pdipm_st(N, n_iter, in, out, NULL);
 }
 
 /* -------------------------------------------------------------- batched wrappers --- */
@@ -688,7 +708,8 @@ int oracle_qp_former_batch(int N, int B, const double *const in[17], double *con
   return bad;
 }
 
-int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], double *const out[6], int nthreads) {
+int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], double *const out[6], int nthreads,
+                       int *status) {
   if (N < 1 || N > MAXN || !g_pat[N].set) return -1;
   if (build_kkt_symbolic(N)) return -1;
   const pattern_t *P = &g_pat[N];
@@ -704,15 +725,15 @@ int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], dou
     double *po[6];
     for (int i = 0; i < 10; ++i) pi[i] = in[i] + (size_t)e * innz[i];
     for (int i = 0; i < 6; ++i) po[i] = out[i] + (size_t)e * onnz[i];
-    bad |= oracle_pdipm(N, n_iter, pi, po) != 0;
+    bad |= oracle_pdipm_st(N, n_iter, pi, po, status ? status + e : NULL) != 0;
   }
-  return bad;
+  return status ? 0 : bad;
 }
 
 /* The GPU caller's full MPC step per env (mpc_controller_cusadi.py:99-169): qp_former, then
  * x = 0, s = max(d - G.0, 1), z = 1, y = y0, then n_iter Newton iterations. */
 int oracle_mpc_solve_batch(int N, int n_iter, double y0, int B, const double *const in[17],
-                           double *const out[6], int nthreads) {
+                           double *const out[6], int nthreads, int *status) {
   if (N < 1 || N > MAXN || !g_pat[N].set) return -1;
   if (build_kkt_symbolic(N)) return -1;
   const pattern_t *P = &g_pat[N];
@@ -741,8 +762,8 @@ int oracle_mpc_solve_batch(int N, int n_iter, double y0, int B, const double *co
     const double *si[10] = {H, G, A, f, d, b, x, s, z, y};
     double *so[6];
     for (int i = 0; i < 6; ++i) so[i] = out[i] + (size_t)e * onnz[i];
-    bad |= oracle_pdipm(N, n_iter, si, so) != 0;
+    bad |= oracle_pdipm_st(N, n_iter, si, so, status ? status + e : NULL) != 0;
     free(H); free(f); free(A); free(b); free(G); free(d); free(x); free(s); free(z); free(y); free(Gx);
   }
-  return bad;
+  return status ? 0 : bad;
 }

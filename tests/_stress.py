@@ -26,8 +26,9 @@ STRESS_CASES = {
     "tilt_N10": (10, dict(tilt=0.6, random_gait=True, residuals=True)),
     # residual accelerations of std 3 m/s^2 / 3 rad/s^2 (6x the SURVEY spread), randomized gait
     "push_N20": (20, dict(random_gait=True, residuals=True, residual_scale=3.0)),
-    # horizons without a register kernel (the runtime-N LDS-resident kernel under the auto path):
-    # flight at N = 5, and the right foot in swing over a 32-stage horizon with tilt and residuals
+    # two more horizons (the regN register kernels under the auto path, the runtime-N LDS-resident
+    # kernel under "lds"): flight at N = 5, and the right foot in swing over a 32-stage horizon with
+    # tilt and residuals
     "flight_N5": (5, dict(contact_override=_contact(STRESS_B, 5, 0, 0))),
     "swing_right_N32": (32, dict(contact_override=_contact(STRESS_B, 32, 1, 0), tilt=0.3, residuals=True)),
 }

@@ -3,8 +3,8 @@ both-sided rows), one foot in swing for the whole horizon, large tilt, large RL 
 HIP step against the oracle at K = 10 and 20 on every env, at the SOLVER_CASES tolerance or 4x the
 per-env FP64 floor between the two CPU restatements (sparse LDL^T oracle vs dense LU,
 tests/golden/make_stress_floor.py), whichever is larger. Every case runs under each solver path:
-"auto" (the fused register kernel at N = 10 / 20, the runtime-N LDS-resident kernel at N = 5 / 32),
-"lds" (the LDS-resident stage-invariant kernel, N = 10 / 20) and "general" (the CCS-table kernel)."""
+"auto" (the fused one-launch register kernel: every horizon 2..32), "lds" (former + the LDS-resident
+stage-invariant kernel, pdipm_srbd_kernel, at every horizon) and "general" (the CCS-table kernel)."""
 import os
 
 import numpy as np
@@ -32,8 +32,6 @@ def _gpu():
 def test_stress_parity(name, path):
     from biped_pympc_amd import _native
     N, wl = stress_workload(name)
-    if path == "lds" and N not in (10, 20):
-        pytest.skip("the auto path already runs the LDS-resident kernel at this horizon")
     floor = np.load(FLOOR)
     ins = [torch.from_numpy(a).cuda() for a in wl.inputs]
     for K in STRESS_K:

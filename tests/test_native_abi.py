@@ -94,3 +94,31 @@ def test_bad_arguments_return_errors_without_touching_the_gpu():
     assert L.srbd_mpc_step(10, 20, 4, 1.0, None, None, None, None, 0, None, None, None, None) != 0
     assert L.srbd_mpc_step(10, 20, 4, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) != 0
     assert L.srbd_mpc_step(10, 20, 0, 1.0, ctypes.byref(prep), None, None, None, 0, None, None, None, None) == 0
+
+
+def test_build_id_is_the_source_hash():
+    """Build provenance: libsrbd_mpc.so carries the hash of the sources and flags it was compiled
+    from (build.py source_hash), readable both from the file and through srbd_build_id(); the drop-in
+    shims carry the id of their own configuration over that core."""
+    build.build()
+    core = _native.lib_path()
+    h = build.source_hash()
+    assert build.embedded_id(core) == h
+    L = ctypes.CDLL(core)
+    L.srbd_build_id.restype = ctypes.c_char_p
+    assert L.srbd_build_id().decode() == h
+    for fn, N, K in build.DROPIN_CONFIGS:
+        path = os.path.join(build.LIB_DIR, build.dropin_lib_name(fn, N, K))
+        assert build.embedded_id(path) == build._shim_hash(fn, N, K, h)
+
+
+def test_source_hash_tracks_content_not_mtime(tmp_path):
+    """A touched source keeps the id; one edited byte changes it (build() rebuilds on a mismatch)."""
+    srcs = build.core_sources()
+    copy = tmp_path / os.path.basename(srcs[-1])
+    copy.write_bytes(open(srcs[-1], "rb").read())
+    h0 = build.source_hash(srcs[:-1] + [str(copy)])
+    os.utime(copy, (1, 1))
+    assert build.source_hash(srcs[:-1] + [str(copy)]) == h0
+    copy.write_bytes(copy.read_bytes() + b" ")
+    assert build.source_hash(srcs[:-1] + [str(copy)]) != h0
