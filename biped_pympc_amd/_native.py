@@ -190,5 +190,12 @@ def build_id() -> str:
         return "unknown"
 
 
+def prepare_device() -> None:
+    """srbd_prepare_device() on the current HIP device: allocate the solver's per-device pool now.
+    Call it before capturing a solver call in a HIP graph (the first solver call on a device
+    allocates it otherwise, which a capture does not allow)."""
+    check(lib().srbd_prepare_device(), "srbd_prepare_device")
+
+
 def last_error() -> str:
     return lib().srbd_last_error().decode(errors="replace")

@@ -41,7 +41,8 @@ struct SolverArgs {
                   // 2: x = input 6, s = max(h - G x, 1), z = 1, y = 0 (_ccs init)
   double y0;
   // the library's per-device pool for QPs the stage-invariant kernels cannot take: scratch_slots
-  // slots of SolverLayout(kMaxN).total doubles, each guarded by a lock word (0 = free)
+  // slots of SolverLayout(kMaxN).total doubles, each guarded by a lock word (0 = free) at
+  // scratch_locks[slot * kLockStride] (one 128-byte line per lock: no false sharing between slots)
   double* scratch;
   int* scratch_locks;
   int scratch_slots;
@@ -53,6 +54,7 @@ struct SolverArgs {
 // mu; bit 1 a combined-direction step length (primal or dual) at its 1e-12 floor in the last
 // iteration; bit 2 the QP was not stage-invariant and took the general solve (scratch fallback).
 constexpr int kStatusNonFinite = 1, kStatusStepFloor = 2, kStatusFallback = 4;
+constexpr int kLockStride = 32;  // ints between two slots' lock words
 __device__ __forceinline__ bool not_finite(double v) { return !__builtin_isfinite(v); }
 
 // iterative-refinement steps per direction in the LDS-resident and general kernels (the register
@@ -634,8 +636,14 @@ struct SolverCtx {
 // a slot of the library's global scratch pool when a stage-invariant kernel meets a QP it cannot
 // take). `lane` >= 64 marks an idle lane (the second wave of a two-wave QP): it takes part in every
 // barrier and stores nothing.
+// `smem`: the QP's working set (the workgroup's LDS in pdipm_kernel, a scratch-pool slot in global
+// memory for the fallback). `lds`, `lds_cap`: LDS the caller can spare (the fallback: the stage-invariant
+// kernel's own LDS, unused by a QP it hands over); the arrays the sequential chains touch go there first
+// -- the factor blocks, their scratch, the solve chains' vectors -- then the row-parallel ones, as long
+// as they fit; the rest stay in `smem`. (Global-memory latency on every chain step is what made the
+// fallback ~2x slower than the same solve in LDS.)
 __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in,
-                                                 int status_bits = 0) {
+                                                 int status_bits = 0, double* lds = nullptr, int lds_cap = 0) {
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;
@@ -645,13 +653,26 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   C.p = 14 * N;
   C.nd = 12 * N;
   C.lane = lane_in;
-  C.AV = smem + Lo.AV; C.GV = smem + Lo.GV; C.HV = smem + Lo.HV;
-  C.X = smem + Lo.X; C.S = smem + Lo.S; C.Z = smem + Lo.Z; C.Y = smem + Lo.Y;
-  C.RX = smem + Lo.RX; C.RS = smem + Lo.RS; C.RE = smem + Lo.RE;
-  C.SI = smem + Lo.SI; C.WD = smem + Lo.WD; C.DI = smem + Lo.DI; C.R2 = smem + Lo.R2; C.VV = smem + Lo.VV;
-  C.PH = smem + Lo.PH; C.DV = smem + Lo.DV; C.R1T = smem + Lo.R1T; C.TV = smem + Lo.TV;
-  C.QV = smem + Lo.QV; C.WV = smem + Lo.WV; C.DS = smem + Lo.DS; C.DZ = smem + Lo.DZ; C.DY = smem + Lo.DY;
-  C.SC = smem + Lo.SC;
+  {
+    int used = 0;
+    auto place = [&](double*& ptr, int off, int n) {
+      const int n2 = (n + 1) & ~1;
+      if (lds && used + n2 <= lds_cap) {
+        ptr = lds + used;
+        used += n2;
+      } else {
+        ptr = smem + off;
+      }
+    };
+    const int nz = C.nz, m = C.m, p = C.p, nd = C.nd;
+    place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 160); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
+    place(C.PH, Lo.PH, 24 * N); place(C.TV, Lo.TV, nz); place(C.R1T, Lo.R1T, nz);
+    place(C.DI, Lo.DI, m); place(C.WD, Lo.WD, m); place(C.SI, Lo.SI, m); place(C.VV, Lo.VV, m);
+    place(C.R2, Lo.R2, m); place(C.DS, Lo.DS, m); place(C.DZ, Lo.DZ, m); place(C.DY, Lo.DY, p);
+    place(C.X, Lo.X, nz); place(C.S, Lo.S, m); place(C.Z, Lo.Z, m); place(C.Y, Lo.Y, p);
+    place(C.RX, Lo.RX, nz); place(C.RS, Lo.RS, m); place(C.RE, Lo.RE, p);
+    place(C.HV, Lo.HV, nz); place(C.GV, Lo.GV, 28 * N); place(C.AV, Lo.AV, 122 * N - 24);
+  }
   const int lane = C.lane, nz = C.nz, m = C.m, p = C.p;
   const int nA = nnz_A(N), nG = 28 * N;
   const double* Hg = solver_in(args, 0) + (size_t)env * nz;
@@ -779,32 +800,35 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
 __device__ __forceinline__ const SolverArgs& kernel_args() {
   return *(const SolverArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // constant -> generic address space
 }
-// `xchg`: an LDS int of the calling workgroup through which a multi-wave QP's waves agree on the slot
-// (wave 0 takes it; the other waves run the solve as idle lanes but read the slot's memory, so they
-// must see the same one); null for a one-wave QP.
+// `lds` / `lds_doubles`: the calling workgroup's LDS (all of it: the QP handed over never started the
+// fast path); its first int is where a multi-wave QP's waves agree on the slot (wave 0 takes it; the
+// other waves run the solve as idle lanes but read the slot's memory, so they must see the same one),
+// the rest holds the chain arrays of the general solve (pdipm_general_at). The pool has as many slots
+// as the device holds resident workgroups of any stage-invariant kernel, so a slot is free at the first
+// or an early probe and no workgroup waits on another's solve.
 template <int kTag>
-__device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs& args, int env, int* xchg) {
+__device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs& args, int env, double* lds,
+                                                                int lds_doubles) {
   const int n = args.scratch_slots;
   int slot = env % n;
+  int* xchg = reinterpret_cast<int*>(lds);
   if (threadIdx.x == 0) {
-    while (atomicCAS(&args.scratch_locks[slot], 0, 1) != 0) {
+    while (atomicCAS(&args.scratch_locks[(size_t)slot * kLockStride], 0, 1) != 0) {
       slot = slot + 1 == n ? 0 : slot + 1;
       __builtin_amdgcn_s_sleep(8);
     }
-    if (xchg) *xchg = slot;
+    *xchg = slot;
   }
-  if (xchg) {
-    __syncthreads();
-    slot = *xchg;
-  } else {
-    slot = __shfl(slot, 0, 64);
-  }
+  __syncthreads();
+  slot = *xchg;
+  __syncthreads();  // every wave has the slot before the general solve reuses the LDS
   __threadfence();
   const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
-  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane, kStatusFallback);
+  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane, kStatusFallback,
+                   lds, lds_doubles);
   __syncthreads();
   __threadfence();
-  if (threadIdx.x == 0) atomicExch(&args.scratch_locks[slot], 0);
+  if (threadIdx.x == 0) atomicExch(&args.scratch_locks[(size_t)slot * kLockStride], 0);
 }
 
 #ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again

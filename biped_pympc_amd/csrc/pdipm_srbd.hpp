@@ -895,7 +895,8 @@ __global__ __launch_bounds__(64) void pdipm_srbd_kernel(SolverArgs args) {
   for (int e = lane; e < nz; e += 64) bad |= !(Hg[e] == Hg[(e < 12 * N ? 0 : 12 * N) + e % 12]);
   const bool any_bad = __any(bad);
   if (any_bad) {
-    pdipm_general_scratch<100 + NT>(kernel_args(), env, nullptr);  // the kernel's sole argument
+    // the kernel's sole argument; its dynamic LDS (FastLayout(N).total doubles) hosts the chain arrays
+    pdipm_general_scratch<100 + NT>(kernel_args(), env, smem, Lo.total);
     return;
   }
   // ---- per-QP constants ----

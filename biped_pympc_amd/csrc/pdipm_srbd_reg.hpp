@@ -357,10 +357,10 @@ __device__ __forceinline__ double grow4(const double* gf, int k, const double* x
   return g[o] * xu[foot_colj(f, o)] + g[2] * xu[foot_colj(f, 2)];
 }
 
-// kFReg: every entry of f and b this lane uses held in registers (the fused kernel, which computes
-// them); false: f's slots t >= 1 and b's x-moment slot are re-read from memory (L2) each iteration --
-// the CCS kernel, whose stage-invariance check and three iterate initialisations leave no room for
-// them: held, they spilled 4 VGPRs (scratch reloads in the Newton loop)
+// kFReg: every entry of f, b and h this lane uses held in registers (the fused kernel, which computes
+// them); false: f's slots t >= 1, b's x-moment slot and h's last slot are re-read from memory (L2)
+// each iteration -- the CCS kernel, whose stage-invariance check, three iterate initialisations and
+// fallback call leave no room for them: held, they spilled 2-4 VGPRs (scratch reloads in the loop)
 template <int N, bool kFReg = true>
 struct RegCtx {
   static constexpr int TPB = reg_tpb(N);
@@ -422,8 +422,10 @@ struct RegCtx {
       bvr[t] = bg[q.valid ? q.e : 0];
     }
 #pragma unroll
-    for (int t = 0; t < SI; ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
+    for (int t = 0; t < (kFReg ? SI : SI - 1); ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
   }
+  // h of slot t (the CCS kernel re-reads its last slot from memory, see kFReg)
+  __device__ double hval(int t, int q) const { return (kFReg || t < SI - 1) ? hvr[t] : hg[q]; }
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
   double e3r[SI];  // the affine refinement's row-3 residuals (degenerate iterations only)
   PROF_DECL
@@ -560,7 +562,7 @@ struct RegCtx {
       if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q >> 4, k = q & 15;
         const double v = grow4(Gf, k, X + nx + m24(i, 12));
-        rs[t] = (v + s[t]) - hv[t];
+        rs[t] = (v + s[t]) - ((kFReg || t < SI - 1) ? hv[t] : hg[q]);
         sz += s[t] * z[t];
       }
     }
@@ -1439,8 +1441,8 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       qp_sync<TPB>();  // RED is reused by the first block reduction
     }
     if (bad) {  // not stage-invariant: the general solve, in this launch (pdipm_general_scratch)
-      // the kernel's sole argument; a multi-wave QP's waves agree on the slot through the DMY sink
-      pdipm_general_scratch<N>(kernel_args(), env, TPB > 64 ? reinterpret_cast<int*>(smem + Lo::DMY) : nullptr);
+      // the kernel's sole argument; the QP's LDS holds the slot hand-over and the chain arrays
+      pdipm_general_scratch<N>(kernel_args(), env, smem, Lo::total);
       return;
     }
   }
@@ -1502,7 +1504,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
-        C.s[t] = fmax(C.hvr[t] - ccs_gx(solver_in(args, 1) + (size_t)env * 28 * N, q, X + nx), 1.0);
+        C.s[t] = fmax(C.hval(t, q) - ccs_gx(solver_in(args, 1) + (size_t)env * 28 * N, q, X + nx), 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
       }
@@ -1530,7 +1532,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     for (int t = 0; t < SI; ++t) {
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
-        C.s[t] = fmax(C.hvr[t] - 0.0, 1.0);
+        C.s[t] = fmax(C.hval(t, q) - 0.0, 1.0);
         C.z[t] = 1.0;
         Z[q] = 1.0;
       }

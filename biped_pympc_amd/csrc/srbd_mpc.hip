@@ -43,7 +43,9 @@ int set_error(int code, const char* what) {
 
 constexpr int kFormerWaves = 4;
 constexpr int kErrInvalid = (int)hipErrorInvalidValue;
-constexpr int kScratchSlots = 256;  // general solves of non-stage-invariant QPs in flight per device
+// general solves of non-stage-invariant QPs in flight per device: one slot per workgroup the device
+// can hold resident of any stage-invariant kernel (at most 8 QPs per CU: the N <= 10 register kernels)
+constexpr int kMaxQpsPerCu = 8;
 
 bool horizon_ok(int N) { return N >= 1 && N <= srbd::kMaxN; }
 
@@ -90,11 +92,15 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 }
 
 // The per-device scratch pool of the stage-invariant solver kernels (pdipm.hpp
-// pdipm_general_scratch): kScratchSlots slots of SolverLayout(kMaxN) doubles (~39 MB) and their lock
-// words, allocated on the first stage-invariant solver call on a device and kept for the process.
+// pdipm_general_scratch): CUs x kMaxQpsPerCu slots of SolverLayout(kMaxN) doubles (2048 slots, ~324 MB
+// of the 288 GB on an MI355X) and their lock words, one per 128-byte line, allocated on the first
+// stage-invariant solver call on a device (or srbd_prepare_device) and kept for the process. With a
+// slot for every resident workgroup no fallback solve waits for another: a batch of QPs that are all
+// not stage-invariant runs at the general solve's rate instead of queueing on a few slots.
 struct ScratchPool {
   double* buf = nullptr;
   int* locks = nullptr;
+  int slots = 0;
 };
 srbd::PerDevice<ScratchPool> g_scratch;
 std::mutex g_scratch_mu;
@@ -118,11 +124,15 @@ ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
       return nullptr;
     }
     const size_t per_slot = (size_t)srbd::SolverLayout(srbd::kMaxN).total;
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int slots = (e == hipSuccess && cus > 0 ? cus : 256) * kMaxQpsPerCu;
+    const size_t lock_ints = (size_t)slots * srbd::kLockStride;
     double* buf = nullptr;
     int* locks = nullptr;
-    hipError_t e = hipMalloc(&buf, sizeof(double) * per_slot * kScratchSlots);
-    if (e == hipSuccess) e = hipMalloc(&locks, sizeof(int) * kScratchSlots);
-    if (e == hipSuccess) e = hipMemset(locks, 0, sizeof(int) * kScratchSlots);
+    if (e == hipSuccess) e = hipMalloc(&buf, sizeof(double) * per_slot * slots);
+    if (e == hipSuccess) e = hipMalloc(&locks, sizeof(int) * lock_ints);
+    if (e == hipSuccess) e = hipMemset(locks, 0, sizeof(int) * lock_ints);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
       (void)hipFree(buf);
@@ -132,6 +142,7 @@ ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
     }
     pool->buf = buf;
     pool->locks = locks;
+    pool->slots = slots;
   }
   return pool;
 }
@@ -142,7 +153,7 @@ int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
   if (!pool) return rc;
   a.scratch = pool->buf;
   a.scratch_locks = pool->locks;
-  a.scratch_slots = kScratchSlots;
+  a.scratch_slots = pool->slots;
   return 0;
 }
 

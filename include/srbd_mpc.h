@@ -132,7 +132,7 @@ int srbd_set_solver_path(int path);
 int srbd_get_solver_path(void);
 
 /* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the
- * stage-invariant kernels (256 slots, ~39 MB of HBM, plus their lock words) -- on the current HIP
+ * stage-invariant kernels (one slot per resident workgroup -- 2048 on an MI355X, ~324 MB of HBM -- plus their lock words) -- on the current HIP
  * device, synchronising it. Optional: the first srbd_pdipm* / srbd_mpc_solve* / evaluate call on a
  * device does the same, but that first call must then not be made inside a stream capture (it returns
  * an error there): call this, or make one ordinary call, before capturing a graph. Returns 0 or an

@@ -3,6 +3,6 @@ cd /root/repo
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-controller > gpurun_out/bench_prof.json 2>gpurun_out/prof.err && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --kernel-reps 2 > gpurun_out/pmc1.json 2>gpurun_out/pmc1.err && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --kernel-reps 2 > gpurun_out/pmc2.json 2>gpurun_out/pmc2.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-controller --no-dropin > gpurun_out/bench_prof.json 2>gpurun_out/prof.err && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --kernel-reps 2 > gpurun_out/pmc1.json 2>gpurun_out/pmc1.err && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --kernel-reps 2 > gpurun_out/pmc2.json 2>gpurun_out/pmc2.err

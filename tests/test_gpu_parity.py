@@ -459,3 +459,31 @@ def test_fused_step_qp_vectors_only_on_request(N):
     views = bufs.qp_views()
     for k in (1, 3, 5):  # f, b, d
         assert torch.equal(views[k], qp[k]), k
+
+
+def test_solver_call_captured_in_a_hip_graph():
+    """srbd_pdipm (stage-invariant kernel with its in-launch fallback) captured in a HIP graph after
+    srbd_prepare_device(): the replay gives the eager call's bits (include/srbd_mpc.h: the pool must
+    exist before a capture)."""
+    from biped_pympc_amd import _native
+    _native.prepare_device()
+    N, K, B = 10, 5, 64
+    wl = make_workload(B, N, seed=81)
+    qp = _cuda(oracle.qp_former(N, wl.inputs))
+    sol_qp = [qp[0], qp[4], qp[2], qp[1], qp[5], qp[3]]
+    eager = [t.clone() for t in solver.pdipm(sol_qp, None, N, K)]
+    out = solver._alloc_solver_outputs(B, N, "cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        solver.pdipm(sol_qp, None, N, K, outputs=out)  # warm-up on the capture's side stream
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        solver.pdipm(sol_qp, None, N, K, outputs=out)
+    for t in out:
+        t.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for k in range(6):
+        assert torch.equal(out[k], eager[k]), k
