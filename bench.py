@@ -597,6 +597,8 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "parity": parity,
             "controller_step": ctrl,
+            # the reference caller's own schedule through the CusADi-ABI drop-ins (INTEGRATION.md option A)
+            "dropin_step_ms": None if dropin is None else dropin["literal_ms"],
             "dropin_step": dropin,
         }
         emit(line)

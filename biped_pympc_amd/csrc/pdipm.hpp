@@ -128,6 +128,20 @@ __device__ inline double ccs_gx(const double* Gv, int q, const double* xu) {
   return acc;
 }
 
+// A call to one phase of the general solve: inlined into the general kernel (kInl: the whole solve is
+// one function, so its working set is known to be LDS -- ds_read / ds_write -- instead of flat accesses
+// through a context object kept in scratch: 1,059 flat loads and 247 scratch accesses before), a real
+// call in the in-launch fallback of the stage-invariant kernels (inlined there, the solve would need
+// ~370 VGPRs under their 256-register budget and clobber every VGPR across the call).
+#define SRBD_GCALL(...)                          \
+  do {                                           \
+    if constexpr (kInl) {                        \
+      [[clang::always_inline]] __VA_ARGS__;      \
+    } else {                                     \
+      __VA_ARGS__;                               \
+    }                                            \
+  } while (0)
+
 struct SolverCtx {
   int N, nz, m, p, nd, lane;
   double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,
@@ -607,14 +621,15 @@ struct SolverCtx {
 
   // kRefineSteps refinement steps (pdipm_srbd.hpp FastCtx::refine: later steps restore the original
   // right-hand side and refine from the full dy = saved + correction)
+  template <bool kInl>
   __device__ void refine() {
     for (int step = 0; step < kRefineSteps; ++step) {
       if (step > 0) {
         for (int e = lane; e < p; e += 64) DY[e] = ysg[e] + DY[e];
-        residuals();
+        SRBD_GCALL(residuals());
       }
-      refine_rhs();
-      solve(true);
+      SRBD_GCALL(refine_rhs());
+      SRBD_GCALL(solve(true));
     }
   }
 
@@ -642,6 +657,7 @@ struct SolverCtx {
 // -- the factor blocks, their scratch, the solve chains' vectors -- then the row-parallel ones, as long
 // as they fit; the rest stay in `smem`. (Global-memory latency on every chain step is what made the
 // fallback ~2x slower than the same solve in LDS.)
+template <bool kInl>
 __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in,
                                                  int status_bits = 0, double* lds = nullptr, int lds_cap = 0) {
   const int N = args.N;
@@ -711,7 +727,8 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
   bool floor_hit = false;
   for (int it = 0; it < args.n_iter; ++it) {
-    const double mu = C.residuals();
+    double mu;
+    SRBD_GCALL(mu = C.residuals());
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
       double a = 0.0, b = 0.0, c = 0.0;
       for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
@@ -721,14 +738,16 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
-    C.factor();
+    SRBD_GCALL(C.factor());
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
-    C.solve();
-    C.refine();  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
-    C.residuals();  // restores RX, RS, RE for the combined solve
-    const double ap = C.step_length(C.S, C.DS), ad = C.step_length(C.Z, C.DZ);
+    SRBD_GCALL(C.solve());
+    SRBD_GCALL(C.template refine<kInl>());  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
+    SRBD_GCALL(C.residuals());  // restores RX, RS, RE for the combined solve
+    double ap, ad;
+    SRBD_GCALL(ap = C.step_length(C.S, C.DS));
+    SRBD_GCALL(ad = C.step_length(C.Z, C.DZ));
     double sza = 0.0;
     for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
     const double mu_aff = wave_sum(sza) / m;
@@ -740,9 +759,11 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q])) + -(C.SI[q] * rc);
     }
     __syncthreads();
-    C.solve();
-    C.refine();
-    const double apc = C.step_length(C.S, C.DS), adc = C.step_length(C.Z, C.DZ);
+    SRBD_GCALL(C.solve());
+    SRBD_GCALL(C.template refine<kInl>());
+    double apc, adc;
+    SRBD_GCALL(apc = C.step_length(C.S, C.DS));
+    SRBD_GCALL(adc = C.step_length(C.Z, C.DZ));
     floor_hit = apc <= 1e-12 || adc <= 1e-12;  // the last iteration's value is reported
     __syncthreads();
     double szn = 0.0;
@@ -824,8 +845,8 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
   __syncthreads();  // every wave has the slot before the general solve reuses the LDS
   __threadfence();
   const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
-  pdipm_general_at(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane, kStatusFallback,
-                   lds, lds_doubles);
+  pdipm_general_at<false>(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane,
+                          kStatusFallback, lds, lds_doubles);
   __syncthreads();
   __threadfence();
   if (threadIdx.x == 0) atomicExch(&args.scratch_locks[(size_t)slot * kLockStride], 0);
@@ -835,7 +856,7 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
 // One workgroup per QP (the "general" solver path, srbd_set_solver_path(1))
 __global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  if ((int)blockIdx.x < args.batch) pdipm_general_at(args, blockIdx.x, smem, threadIdx.x);
+  if ((int)blockIdx.x < args.batch) pdipm_general_at<true>(args, blockIdx.x, smem, threadIdx.x);
 }
 #endif  // SRBD_NO_GENERAL_KERNEL
 

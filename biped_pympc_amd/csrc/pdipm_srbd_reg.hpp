@@ -1396,7 +1396,6 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     C.fg = solver_in(args, 3) + (size_t)env * nz;
     C.hg = solver_in(args, 4) + (size_t)env * m;
     C.bg = solver_in(args, 5) + (size_t)env * p;
-    C.load_qp_vectors();
     // ---- compact load (stage 0/1 slices) ----
     for (int e = lane; e < 144; e += TPB) {
       const int r = e / 12, j = e % 12;
@@ -1409,10 +1408,6 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       Pd[lane] = Ag[a_pidx(c_tab, N, 0, lane)];
       Hu[lane] = Hg[nx + lane];
       Hu[12 + lane] = Hg[lane];
-    }
-    if (lane == 0) {
-      e6 = Ag[a_ubase(N) + c_tab.e6];
-      e9 = Ag[a_ubase(N) + c_tab.e9];
     }
     qp_sync<TPB>();
     if (lane < 28) Gf[g_row(c_tab.grow[lane]) + foot_pos(c_tab.gcol[lane])] = Gg[lane];
@@ -1444,6 +1439,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       // the kernel's sole argument; the QP's LDS holds the slot hand-over and the chain arrays
       pdipm_general_scratch<N>(kernel_args(), env, smem, Lo::total);
       return;
+    }
+    // loaded only now: a value held across the fallback call would be saved around it (the callee
+    // clobbers every VGPR), i.e. spill in the fast path too
+    C.load_qp_vectors();
+    if (lane == 0) {
+      e6 = Ag[a_ubase(N) + c_tab.e6];
+      e9 = Ag[a_ubase(N) + c_tab.e9];
     }
   }
   // ---- per-QP constants ----

@@ -59,8 +59,12 @@ def main():
         qp, it = qp_batch(B, N, every)
         st = torch.zeros(B, dtype=torch.int32, device="cuda")
         with _native.solver_path(path):
-            ms = timed(lambda: solver.pdipm(qp, it, N, K, status=st))
-        flagged = int(((st & _native.STATUS_FALLBACK) != 0).sum())
+            try:
+                ms = timed(lambda: solver.pdipm(qp, it, N, K, status=st))
+                flagged = int(((st & _native.STATUS_FALLBACK) != 0).sum())
+            except _native.NativeLibraryMissing:  # an earlier build (SRBD_LIB) without the status word
+                ms = timed(lambda: solver.pdipm(qp, it, N, K))
+                flagged = None
         out[name] = {"ms": round(ms, 4), "qps": B, "fallback_qps": flagged}
         print(name, out[name], file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)

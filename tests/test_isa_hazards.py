@@ -42,11 +42,27 @@ def _isa(tmp_path, unit):
     return outs
 
 
+def _reg_horizon(name):
+    import re
+    m = re.search(r"reg_kernelILi(\d+)E", name)
+    return int(m.group(1)) if m else None
+
+
 @pytest.mark.parametrize("unit", ["srbd_mpc.hip", "srbd_reg20.hip", "srbd_regN.hip"])
 def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
+    """Also, on the same ISA: the register kernels keep every VGPR in registers -- the fused step
+    kernel (mpc_step_reg_kernel) at every horizon up to 24 and the CCS solver kernel
+    (pdipm_srbd_reg_kernel, the CusADi drop-in's path) up to 20 (the three-wave QPs beyond spill a few
+    VGPRs)."""
     from dpp_hazard_check import check
+    from kernel_resources import resources
     for s in _isa(tmp_path, unit):
         assert check(s) == 0, s
+        for name, r in resources(s, "reg_kernel").items():
+            n = _reg_horizon(name)
+            limit = 24 if "mpc_step" in name else 20
+            if n is not None and n <= limit:
+                assert r["vgpr_spill_count"] == 0, (name, r)
 
 
 def test_checker_detects_planted_hazards(tmp_path):
