@@ -41,11 +41,12 @@ struct SolverArgs {
                   // 2: x = input 6, s = max(h - G x, 1), z = 1, y = 0 (_ccs init)
   double y0;
   // the library's per-device pool for QPs the stage-invariant kernels cannot take: scratch_slots
-  // slots of SolverLayout(kMaxN).total doubles, each guarded by a lock word (0 = free) at
+  // slots of scratch_stride doubles, each guarded by a lock word (0 = free) at
   // scratch_locks[slot * kLockStride] (one 128-byte line per lock: no false sharing between slots)
   double* scratch;
   int* scratch_locks;
   int scratch_slots;
+  int scratch_stride;  // doubles per slot: the largest SolverLayout(N).total over N = 1..kMaxN
   int* status;  // (batch) per-problem status word (kStatus* bits), or null: not written
 };
 
@@ -69,10 +70,12 @@ __device__ inline double* solver_out(const SolverArgs& a, int i) {
   return a.dev_out ? a.dev_out[i] : a.out[i];
 }
 
+constexpr int kTablesDoubles = (int)((sizeof(Tables) + 15) / 16) * 2;
+
 // LDS carve (doubles) for horizon N; every offset is a multiple of 2 doubles (16 B).
 struct SolverLayout {
   int AV, GV, HV, X, S, Z, Y, RX, RS, RE, SI, WD, DI, R2, VV, PH, DV, R1T, TV, QV, WV, DS, DZ, DY, SC,
-      total;
+      TB, CV, total;
   __host__ __device__ SolverLayout(int N) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
     int o = 0;
@@ -86,6 +89,10 @@ struct SolverLayout {
     QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
     SC = take(160);
+    TB = take(kTablesDoubles);  // a copy of c_tab: the index tables, read with lane-varying indices
+    // the dual couplings S_{i,i-1} over x_i's 36-value block (Ssub), where they still fit the 160 KiB
+    // of LDS a workgroup may have (all horizons but 32; without them Ssub is formed on the fly)
+    CV = (o + 36 * N) * 8 <= 160 * 1024 ? take(36 * N) : -1;
     total = o;
   }
 };
@@ -148,25 +155,39 @@ struct SolverCtx {
       *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
   double *xsg, *ysg;  // this QP's x / y output rows: the saved dx / dy during the refinement solve
+  // the index tables (a copy of c_tab in LDS where one fits: its lookups take lane-varying indices,
+  // which from constant memory are vector loads of L2 latency on every chain step) and the couplings
+  double* CV;
+  const Tables* T;
 
   // ---- structured access to the CCS values (stage-periodic tables) ----
-  __device__ double Pv(int i, int r) const { return AV[a_pidx(c_tab, N, i, r)]; }
+  __device__ double Pv(int i, int r) const { return AV[a_pidx(*T, N, i, r)]; }
   __device__ double Mv(int i, int r, int j) const {  // stage i rows x x_i columns, i >= 1
-    const int o = c_tab.Mi[r][j];
+    const int o = T->Mi[r][j];
     return o >= 0 ? AV[a_xblock(i) + o] : 0.0;
   }
   __device__ double Nv(int i, int r, int j) const {
-    const int o = c_tab.Ni[r][j];
+    const int o = T->Ni[r][j];
     return o >= 0 ? AV[a_ublock(N, i) + o] : 0.0;
   }
-  __device__ double E6(int i) const { return AV[a_ublock(N, i) + c_tab.e6]; }
-  __device__ double E9(int i) const { return AV[a_ublock(N, i) + c_tab.e9]; }
+  __device__ double E6(int i) const { return AV[a_ublock(N, i) + T->e6]; }
+  __device__ double E9(int i) const { return AV[a_ublock(N, i) + T->e9]; }
   __device__ double phix(int k, int j) const { return HV[12 * (k - 1) + j] + kBeta; }  // x_k, k >= 1
   __device__ double phiu(int i, int j) const { return HV[12 * N + 12 * i + j] + kBeta; }
-  // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i)
+  // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i), precomputed
+  // per QP into CV at the offsets of x_i's CCS block (couplings()): no division on the chains
   __device__ double Ssub(int i, int r, int c) const {
-    const int o = c_tab.Mi[r][c];
-    return o >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, c) / phix(i, c) : 0.0;
+    const int o = T->Mi[r][c];
+    if (o < 0) return 0.0;
+    return CV ? CV[a_xblock(i) + o] : AV[a_xblock(i) + o] * Pv(i - 1, c) / phix(i, c);
+  }
+  // CV: the QP's constant couplings (H and A do not change across the Newton iterations)
+  __device__ void couplings() {
+    if (!CV) return;
+    for (int e = lane; e < 36 * (N - 1); e += 64) {
+      const int i = e / 36 + 1, o = e % 36, j = T->xb_j[o];
+      CV[e] = T->xb_r[o] >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, j) / phix(i, j) : 0.0;
+    }
   }
   __device__ double G(int i, int q) const { return GV[28 * i + q]; }
 
@@ -179,20 +200,20 @@ struct SolverCtx {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
         for (int q = 0; q < 28; ++q)
-          if (c_tab.gcol[q] == j) gz += G(i, q) * Z[16 * i + c_tab.grow[q]];
+          if (T->gcol[q] == j) gz += G(i, q) * Z[16 * i + T->grow[q]];
         double ay = 0.0;
-        const int ub = a_ublock(N, i) + c_tab.cpu[j];
-        for (int t = 0; t < c_tab.su_n[j]; ++t) ay += AV[ub + t] * Y[12 * i + c_tab.su[j][t]];
-        if (j == 6) ay += AV[ub + c_tab.su_n[j]] * Y[12 * N + 2 * i];
-        if (j == 9) ay += AV[ub + c_tab.su_n[j]] * Y[12 * N + 2 * i + 1];
+        const int ub = a_ublock(N, i) + T->cpu[j];
+        for (int t = 0; t < T->su_n[j]; ++t) ay += AV[ub + t] * Y[12 * i + T->su[j][t]];
+        if (j == 6) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i];
+        if (j == 9) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
       } else {
         const int k = c / 12 + 1, j = c % 12;
         double ay;
         if (k < N) {
-          const int xb = a_xblock(k) + c_tab.cpx[j];
+          const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * Y[12 * (k - 1) + j];
-          for (int t = 0; t < c_tab.sx_n[j]; ++t) ay += AV[xb + 1 + t] * Y[12 * k + c_tab.sx[j][t]];
+          for (int t = 0; t < T->sx_n[j]; ++t) ay += AV[xb + 1 + t] * Y[12 * k + T->sx[j][t]];
         } else {
           ay = AV[36 * (N - 1) + j] * Y[12 * (k - 1) + j];
         }
@@ -206,12 +227,12 @@ struct SolverCtx {
         const int i = e / 12, r = e % 12;
         if (i >= 1)
           for (int j = 0; j < 12; ++j) {
-            const int o = c_tab.Mi[r][j];
+            const int o = T->Mi[r][j];
             if (o >= 0) v += AV[a_xblock(i) + o] * X[12 * (i - 1) + j];
           }
         v += Pv(i, r) * X[12 * i + r];
         for (int j = 0; j < 12; ++j) {
-          const int o = c_tab.Ni[r][j];
+          const int o = T->Ni[r][j];
           if (o >= 0) v += AV[a_ublock(N, i) + o] * X[12 * N + 12 * i + j];
         }
       } else {
@@ -224,8 +245,8 @@ struct SolverCtx {
     for (int q = lane; q < m; q += 64) {
       const int i = q / 16, k = q % 16;
       double v = 0.0;
-      for (int t = 0; t < c_tab.gr_n[k]; ++t)
-        v += G(i, c_tab.gr_off[k][t]) * X[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      for (int t = 0; t < T->gr_n[k]; ++t)
+        v += G(i, T->gr_off[k][t]) * X[12 * N + 12 * i + T->gr_col[k][t]];
       RS[q] = (v + S[q]) - hg[q];
       sz += S[q] * Z[q];
     }
@@ -251,13 +272,19 @@ struct SolverCtx {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? phiu(i, c_tab.foot_col[f][r]) : 0.0;
+        for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? phiu(i, T->foot_col[f][r]) : 0.0;
       for (int k = 0; k < 8; ++k) {
         const int q = 16 * i + 8 * f + k;
         const double lam = DI[q] * WD[q];
         double g4[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int t = 0; t < c_tab.gr_n[8 * f + k]; ++t)
-          g4[c_tab.col_pos[c_tab.gr_col[8 * f + k][t]]] = G(i, c_tab.gr_off[8 * f + k][t]);
+        const int row = 8 * f + k, nrow = T->gr_n[row];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {  // (at most two entries per row; constant indices into g4: no scratch)
+          const int pos = t < nrow ? T->col_pos[T->gr_col[row][t]] : -1;
+          const double v = t < nrow ? G(i, T->gr_off[row][t]) : 0.0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) g4[b] = pos == b ? v : g4[b];
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -289,7 +316,7 @@ struct SolverCtx {
       }
       if (i >= 1)
         for (int j = 0; j < 12; ++j) {
-          const int o1 = c_tab.Mi[r][j], o2 = c_tab.Mi[c][j];
+          const int o1 = T->Mi[r][j], o2 = T->Mi[c][j];
           if (o1 >= 0 && o2 >= 0) v += AV[a_xblock(i) + o1] * AV[a_xblock(i) + o2] / phix(i, j);
         }
 #pragma unroll
@@ -297,8 +324,8 @@ struct SolverCtx {
         double vr[4], vc[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          vr[a] = Nv(i, r, c_tab.foot_col[f][a]);
-          vc[a] = Nv(i, c, c_tab.foot_col[f][a]);
+          vr[a] = Nv(i, r, T->foot_col[f][a]);
+          vc[a] = Nv(i, c, T->foot_col[f][a]);
         }
         const double* ph = PH + 24 * i + 10 * f;
 #pragma unroll
@@ -323,7 +350,7 @@ struct SolverCtx {
           const int r = e / 12, c = e % 12;
           double u = 0.0;
           for (int k = 0; k < 12; ++k) {
-            const int o = c_tab.Mi[r][k];
+            const int o = T->Mi[r][k];
             if (o >= 0) u += Ssub(i, r, k) * Dp[sym_idx(k, c)];
           }
           SC[e] = u;
@@ -335,7 +362,7 @@ struct SolverCtx {
           const int c = e - r * (r + 1) / 2;
           double acc = 0.0;
           for (int k = 0; k < 12; ++k)
-            if (c_tab.Mi[c][k] >= 0) acc += SC[r * 12 + k] * Ssub(i, c, k);
+            if (T->Mi[c][k] >= 0) acc += SC[r * 12 + k] * Ssub(i, c, k);
           Di[e] -= acc;
         }
         __syncthreads();
@@ -383,8 +410,8 @@ struct SolverCtx {
     for (int q = lane; q < m; q += 64) {  // step 0 (rows 2 and 3)
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      for (int t = 0; t < c_tab.gr_n[k]; ++t)
-        gd += G(i, c_tab.gr_off[k][t]) * TV[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      for (int t = 0; t < T->gr_n[k]; ++t)
+        gd += G(i, T->gr_off[k][t]) * TV[12 * N + 12 * i + T->gr_col[k][t]];
       const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
       const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
       const double qc = DI[q] * (e2 - WD[q] * e3);
@@ -401,20 +428,20 @@ struct SolverCtx {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
         for (int q = 0; q < 28; ++q)
-          if (c_tab.gcol[q] == j) gz += G(i, q) * DZ[16 * i + c_tab.grow[q]];
+          if (T->gcol[q] == j) gz += G(i, q) * DZ[16 * i + T->grow[q]];
         double ay = 0.0;
-        const int ub = a_ublock(N, i) + c_tab.cpu[j];
-        for (int t = 0; t < c_tab.su_n[j]; ++t) ay += AV[ub + t] * DY[12 * i + c_tab.su[j][t]];
-        if (j == 6) ay += AV[ub + c_tab.su_n[j]] * DY[12 * N + 2 * i];
-        if (j == 9) ay += AV[ub + c_tab.su_n[j]] * DY[12 * N + 2 * i + 1];
+        const int ub = a_ublock(N, i) + T->cpu[j];
+        for (int t = 0; t < T->su_n[j]; ++t) ay += AV[ub + t] * DY[12 * i + T->su[j][t]];
+        if (j == 6) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i];
+        if (j == 9) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
       } else {
         const int k = c / 12 + 1, j = c % 12;
         double ay;
         if (k < N) {
-          const int xb = a_xblock(k) + c_tab.cpx[j];
+          const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * DY[12 * (k - 1) + j];
-          for (int t = 0; t < c_tab.sx_n[j]; ++t) ay += AV[xb + 1 + t] * DY[12 * k + c_tab.sx[j][t]];
+          for (int t = 0; t < T->sx_n[j]; ++t) ay += AV[xb + 1 + t] * DY[12 * k + T->sx[j][t]];
         } else {
           ay = AV[36 * (N - 1) + j] * DY[12 * (k - 1) + j];
         }
@@ -428,12 +455,12 @@ struct SolverCtx {
         const int i = e / 12, r = e % 12;
         if (i >= 1)
           for (int j = 0; j < 12; ++j) {
-            const int o = c_tab.Mi[r][j];
+            const int o = T->Mi[r][j];
             if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
           }
         v += Pv(i, r) * TV[12 * i + r];
         for (int j = 0; j < 12; ++j) {
-          const int o = c_tab.Ni[r][j];
+          const int o = T->Ni[r][j];
           if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
         }
       } else {
@@ -462,7 +489,7 @@ struct SolverCtx {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double g = 0.0;
         for (int q = 0; q < 28; ++q)
-          if (c_tab.gcol[q] == j) g += G(i, q) * VV[16 * i + c_tab.grow[q]];
+          if (T->gcol[q] == j) g += G(i, q) * VV[16 * i + T->grow[q]];
         v -= g;
       }
       R1T[c] = v;
@@ -476,13 +503,13 @@ struct SolverCtx {
       const double* ph = PH + 24 * i + 10 * f;
       double rv[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) rv[a] = R1T[12 * N + 12 * i + c_tab.foot_col[f][a]];
+      for (int a = 0; a < 4; ++a) rv[a] = R1T[12 * N + 12 * i + T->foot_col[f][a]];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         double t = 0.0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * rv[b];
-        TV[12 * N + 12 * i + c_tab.foot_col[f][a]] = t;
+        TV[12 * N + 12 * i + T->foot_col[f][a]] = t;
       }
       } else {
       const int i = task - 2 * N;
@@ -502,12 +529,12 @@ struct SolverCtx {
       double v = 0.0;
       if (i >= 1)
         for (int j = 0; j < 12; ++j) {
-          const int o = c_tab.Mi[r][j];
+          const int o = T->Mi[r][j];
           if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
         }
       v += Pv(i, r) * TV[12 * i + r];
       for (int j = 0; j < 12; ++j) {
-        const int o = c_tab.Ni[r][j];
+        const int o = T->Ni[r][j];
         if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
       }
       QV[e] = v + RE[e];
@@ -519,7 +546,7 @@ struct SolverCtx {
         if (lane < 12) {
           double acc = 0.0;
           for (int k = 0; k < 12; ++k)
-            if (c_tab.Mi[lane][k] >= 0) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
+            if (T->Mi[lane][k] >= 0) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
           QV[12 * i + lane] -= acc;
         }
         __syncthreads();
@@ -539,7 +566,7 @@ struct SolverCtx {
       if (lane < 12) {
         double acc = 0.0;
         for (int r = 0; r < 12; ++r)
-          if (c_tab.Mi[r][lane] >= 0) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
+          if (T->Mi[r][lane] >= 0) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
         SC[lane] = acc;
       }
       __syncthreads();
@@ -556,9 +583,9 @@ struct SolverCtx {
       const int k = c / 12 + 1, j = c % 12;
       double aty;
       if (k < N) {
-        const int xb = a_xblock(k) + c_tab.cpx[j];
+        const int xb = a_xblock(k) + T->cpx[j];
         aty = AV[xb] * QV[12 * (k - 1) + j];
-        for (int t = 0; t < c_tab.sx_n[j]; ++t) aty += AV[xb + 1 + t] * QV[12 * k + c_tab.sx[j][t]];
+        for (int t = 0; t < T->sx_n[j]; ++t) aty += AV[xb + 1 + t] * QV[12 * k + T->sx[j][t]];
       } else {
         aty = AV[36 * (N - 1) + j] * QV[12 * (k - 1) + j];
       }
@@ -570,9 +597,9 @@ struct SolverCtx {
       const int i = foot ? (task >> 1) : task - 2 * N;
       const int b = 12 * N + 12 * i;
       auto aty_u = [&](int j) {
-        const int ub = a_ublock(N, i) + c_tab.cpu[j];
+        const int ub = a_ublock(N, i) + T->cpu[j];
         double a = 0.0;
-        for (int t = 0; t < c_tab.su_n[j]; ++t) a += AV[ub + t] * QV[12 * i + c_tab.su[j][t]];
+        for (int t = 0; t < T->su_n[j]; ++t) a += AV[ub + t] * QV[12 * i + T->su[j][t]];
         return a;
       };
       if (foot) {
@@ -580,13 +607,13 @@ struct SolverCtx {
         const double* ph = PH + 24 * i + 10 * f;
         double av[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) av[a] = aty_u(c_tab.foot_col[f][a]);
+        for (int a = 0; a < 4; ++a) av[a] = aty_u(T->foot_col[f][a]);
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
-          const int o = b + c_tab.foot_col[f][a];
+          const int o = b + T->foot_col[f][a];
           TV[o] = ref ? xsg[o] + (TV[o] - t) : TV[o] - t;
         }
       } else {
@@ -610,8 +637,8 @@ struct SolverCtx {
     for (int q = lane; q < m; q += 64) {
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      for (int t = 0; t < c_tab.gr_n[k]; ++t)
-        gd += G(i, c_tab.gr_off[k][t]) * TV[12 * N + 12 * i + c_tab.gr_col[k][t]];
+      for (int t = 0; t < T->gr_n[k]; ++t)
+        gd += G(i, T->gr_off[k][t]) * TV[12 * N + 12 * i + T->gr_col[k][t]];
       const double dz = VV[q] + DI[q] * WD[q] * gd;
       DZ[q] = dz;
       DS[q] = -RS[q] - gd + kDelta * dz;
@@ -681,6 +708,18 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       }
     };
     const int nz = C.nz, m = C.m, p = C.p, nd = C.nd;
+    double* tb = nullptr;
+    place(tb, Lo.TB, kTablesDoubles);
+    const bool tb_lds = lds == nullptr || tb != smem + Lo.TB;  // an LDS copy (else read c_tab itself)
+    C.T = tb_lds ? reinterpret_cast<const Tables*>(tb) : &c_tab;
+    if (tb_lds) {  // copy the tables, 2 bytes per lane and pass (Tables is 2-byte aligned)
+      static_assert(sizeof(Tables) % 2 == 0 && alignof(Tables) <= 16, "Tables copy");
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(&c_tab);
+      uint16_t* dst = reinterpret_cast<uint16_t*>(tb);
+      for (int w = lane_in; w < (int)(sizeof(Tables) / 2); w += 64) dst[w] = src[w];
+    }
+    if (Lo.CV >= 0) place(C.CV, Lo.CV, 36 * N);
+    else C.CV = nullptr;
     place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 160); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
     place(C.PH, Lo.PH, 24 * N); place(C.TV, Lo.TV, nz); place(C.R1T, Lo.R1T, nz);
     place(C.DI, Lo.DI, m); place(C.WD, Lo.WD, m); place(C.SI, Lo.SI, m); place(C.VV, Lo.VV, m);
@@ -722,6 +761,8 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - 0.0, 1.0); C.Z[e] = 1.0; }
     for (int e = lane; e < p; e += 64) C.Y[e] = args.y0;
   }
+  __syncthreads();
+  C.couplings();
   __syncthreads();
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
@@ -845,7 +886,7 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
   __syncthreads();  // every wave has the slot before the general solve reuses the LDS
   __threadfence();
   const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
-  pdipm_general_at<false>(args, env, args.scratch + (size_t)slot * SolverLayout(kMaxN).total, lane,
+  pdipm_general_at<false>(args, env, args.scratch + (size_t)slot * args.scratch_stride, lane,
                           kStatusFallback, lds, lds_doubles);
   __syncthreads();
   __threadfence();

@@ -5,6 +5,7 @@
 // tables (srbd_common.hpp) are compile-time initialised, so each unit's copy is identical.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -92,7 +93,7 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 }
 
 // The per-device scratch pool of the stage-invariant solver kernels (pdipm.hpp
-// pdipm_general_scratch): CUs x kMaxQpsPerCu slots of SolverLayout(kMaxN) doubles (2048 slots, ~324 MB
+// pdipm_general_scratch): CUs x kMaxQpsPerCu slots of general_slot_doubles() (2048 slots, ~327 MB
 // of the 288 GB on an MI355X) and their lock words, one per 128-byte line, allocated on the first
 // stage-invariant solver call on a device (or srbd_prepare_device) and kept for the process. With a
 // slot for every resident workgroup no fallback solve waits for another: a batch of QPs that are all
@@ -101,7 +102,16 @@ struct ScratchPool {
   double* buf = nullptr;
   int* locks = nullptr;
   int slots = 0;
+  int stride = 0;  // doubles per slot
 };
+
+// doubles one slot needs: the general solve's layout at its largest horizon (not necessarily N = kMaxN:
+// the precomputed couplings are dropped where they would not fit 160 KiB of LDS)
+int general_slot_doubles() {
+  int s = 0;
+  for (int n = 1; n <= srbd::kMaxN; ++n) s = std::max(s, srbd::SolverLayout(n).total);
+  return s;
+}
 srbd::PerDevice<ScratchPool> g_scratch;
 std::mutex g_scratch_mu;
 
@@ -123,7 +133,7 @@ ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
                                   "scratch pool is allocated on first use: call srbd_prepare_device() first)");
       return nullptr;
     }
-    const size_t per_slot = (size_t)srbd::SolverLayout(srbd::kMaxN).total;
+    const size_t per_slot = (size_t)general_slot_doubles();
     int cus = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int slots = (e == hipSuccess && cus > 0 ? cus : 256) * kMaxQpsPerCu;
@@ -143,6 +153,7 @@ ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
     pool->buf = buf;
     pool->locks = locks;
     pool->slots = slots;
+    pool->stride = (int)per_slot;
   }
   return pool;
 }
@@ -154,6 +165,7 @@ int attach_scratch(srbd::SolverArgs& a, hipStream_t s) {
   a.scratch = pool->buf;
   a.scratch_locks = pool->locks;
   a.scratch_slots = pool->slots;
+  a.scratch_stride = pool->stride;
   return 0;
 }
 
