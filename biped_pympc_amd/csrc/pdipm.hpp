@@ -159,6 +159,7 @@ struct SolverCtx {
   // which from constant memory are vector loads of L2 latency on every chain step) and the couplings
   double* CV;
   const Tables* T;
+  PROF_DECL  // diagnostic phase stamps (scripts/general_phase_profile.py); empty in the product build
 
   // ---- structured access to the CCS values (stage-periodic tables) ----
   __device__ double Pv(int i, int r) const { return AV[a_pidx(*T, N, i, r)]; }
@@ -176,10 +177,31 @@ struct SolverCtx {
   __device__ double phiu(int i, int j) const { return HV[12 * N + 12 * i + j] + kBeta; }
   // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i), precomputed
   // per QP into CV at the offsets of x_i's CCS block (couplings()): no division on the chains
+  // Branch-free (a structural zero reads an in-bounds value and returns 0): the callers' 12-term sums
+  // then issue their LDS loads together instead of one exec-masked round trip per term.
   __device__ double Ssub(int i, int r, int c) const {
-    const int o = T->Mi[r][c];
-    if (o < 0) return 0.0;
-    return CV ? CV[a_xblock(i) + o] : AV[a_xblock(i) + o] * Pv(i - 1, c) / phix(i, c);
+    const int o = T->Mi[r][c], oc = o >= 0 ? o : 0;
+    const double v = CV ? CV[a_xblock(i) + oc] : AV[a_xblock(i) + oc] * Pv(i - 1, c) / phix(i, c);
+    return o >= 0 ? v : 0.0;
+  }
+  // (M_i v)_r and (N_i v)_r of stage i (v: 12 entries), branch-free
+  __device__ double mrow(int i, int r, const double* v) const {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int o = T->Mi[r][j];
+      s += (o >= 0 ? AV[a_xblock(i) + (o >= 0 ? o : 0)] : 0.0) * v[j];
+    }
+    return s;
+  }
+  __device__ double nrow(int i, int r, const double* v) const {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int o = T->Ni[r][j];
+      s += (o >= 0 ? AV[a_ublock(N, i) + (o >= 0 ? o : 0)] : 0.0) * v[j];
+    }
+    return s;
   }
   // CV: the QP's constant couplings (H and A do not change across the Newton iterations)
   __device__ void couplings() {
@@ -225,16 +247,9 @@ struct SolverCtx {
       double v = 0.0;
       if (e < 12 * N) {
         const int i = e / 12, r = e % 12;
-        if (i >= 1)
-          for (int j = 0; j < 12; ++j) {
-            const int o = T->Mi[r][j];
-            if (o >= 0) v += AV[a_xblock(i) + o] * X[12 * (i - 1) + j];
-          }
+        if (i >= 1) v += mrow(i, r, X + 12 * (i - 1));
         v += Pv(i, r) * X[12 * i + r];
-        for (int j = 0; j < 12; ++j) {
-          const int o = T->Ni[r][j];
-          if (o >= 0) v += AV[a_ublock(N, i) + o] * X[12 * N + 12 * i + j];
-        }
+        v += nrow(i, r, X + 12 * N + 12 * i);
       } else {
         const int i = (e - 12 * N) / 2, w = (e - 12 * N) % 2;
         v = (w == 0 ? E6(i) * X[12 * N + 12 * i + 6] : E9(i) * X[12 * N + 12 * i + 9]);
@@ -315,9 +330,12 @@ struct SolverCtx {
         v = pr * pr / phix(i + 1, r) + kDelta;
       }
       if (i >= 1)
+#pragma unroll
         for (int j = 0; j < 12; ++j) {
           const int o1 = T->Mi[r][j], o2 = T->Mi[c][j];
-          if (o1 >= 0 && o2 >= 0) v += AV[a_xblock(i) + o1] * AV[a_xblock(i) + o2] / phix(i, j);
+          const bool nz = o1 >= 0 && o2 >= 0;
+          const double t = AV[a_xblock(i) + (nz ? o1 : 0)] * AV[a_xblock(i) + (nz ? o2 : 0)] / phix(i, j);
+          v += nz ? t : 0.0;
         }
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
@@ -341,6 +359,7 @@ struct SolverCtx {
       DV[e] = v;
     }
     __syncthreads();
+    PROF_ADD_CTX((*this), 1);
     // block recursion over stages: D_i = S_ii - S_{i,i-1} D_{i-1}^-1 S_{i,i-1}^T ; DV_i <- D_i^-1
     for (int i = 0; i < N; ++i) {
       double* Di = DV + 78 * i;
@@ -349,10 +368,8 @@ struct SolverCtx {
         for (int e = lane; e < 144; e += 64) {
           const int r = e / 12, c = e % 12;
           double u = 0.0;
-          for (int k = 0; k < 12; ++k) {
-            const int o = T->Mi[r][k];
-            if (o >= 0) u += Ssub(i, r, k) * Dp[sym_idx(k, c)];
-          }
+#pragma unroll
+          for (int k = 0; k < 12; ++k) u += Ssub(i, r, k) * Dp[sym_idx(k, c)];
           SC[e] = u;
         }
         __syncthreads();
@@ -361,8 +378,8 @@ struct SolverCtx {
           while ((r + 1) * (r + 2) / 2 <= e) ++r;
           const int c = e - r * (r + 1) / 2;
           double acc = 0.0;
-          for (int k = 0; k < 12; ++k)
-            if (T->Mi[c][k] >= 0) acc += SC[r * 12 + k] * Ssub(i, c, k);
+#pragma unroll
+          for (int k = 0; k < 12; ++k) acc += SC[r * 12 + k] * Ssub(i, c, k);
           Di[e] -= acc;
         }
         __syncthreads();
@@ -398,6 +415,7 @@ struct SolverCtx {
       if (e1 < 78) Di[e1] = -Di[e1];
       __syncthreads();
     }
+    PROF_ADD_CTX((*this), 2);
   }
 
   // One step of iterative refinement of a direction against the full KKT from the residuals of all
@@ -453,16 +471,9 @@ struct SolverCtx {
       double v = 0.0;
       if (e < 12 * N) {
         const int i = e / 12, r = e % 12;
-        if (i >= 1)
-          for (int j = 0; j < 12; ++j) {
-            const int o = T->Mi[r][j];
-            if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
-          }
+        if (i >= 1) v += mrow(i, r, TV + 12 * (i - 1));
         v += Pv(i, r) * TV[12 * i + r];
-        for (int j = 0; j < 12; ++j) {
-          const int o = T->Ni[r][j];
-          if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
-        }
+        v += nrow(i, r, TV + 12 * N + 12 * i);
       } else {
         const int i = (e - 12 * N) / 2, w = (e - 12 * N) % 2;
         v = (w == 0 ? E6(i) * TV[12 * N + 12 * i + 6] : E9(i) * TV[12 * N + 12 * i + 9]);
@@ -470,6 +481,7 @@ struct SolverCtx {
       RE[e] = (v + RE[e]) - kDelta * DY[e];
     }
     __syncthreads();
+    PROF_ADD_CTX((*this), 7);
   }
 
   // ------------------------------------------------------------------------- solve ----
@@ -527,26 +539,20 @@ struct SolverCtx {
     for (int e = lane; e < 12 * N; e += 64) {
       const int i = e / 12, r = e % 12;
       double v = 0.0;
-      if (i >= 1)
-        for (int j = 0; j < 12; ++j) {
-          const int o = T->Mi[r][j];
-          if (o >= 0) v += AV[a_xblock(i) + o] * TV[12 * (i - 1) + j];
-        }
+      if (i >= 1) v += mrow(i, r, TV + 12 * (i - 1));
       v += Pv(i, r) * TV[12 * i + r];
-      for (int j = 0; j < 12; ++j) {
-        const int o = T->Ni[r][j];
-        if (o >= 0) v += AV[a_ublock(N, i) + o] * TV[12 * N + 12 * i + j];
-      }
+      v += nrow(i, r, TV + 12 * N + 12 * i);
       QV[e] = v + RE[e];
     }
     __syncthreads();
+    PROF_ADD_CTX((*this), 3);
     // forward: q_i -= S_{i,i-1} w_{i-1} ; w_i = D_i^-1 q_i
     for (int i = 0; i < N; ++i) {
       if (i >= 1) {
         if (lane < 12) {
           double acc = 0.0;
-          for (int k = 0; k < 12; ++k)
-            if (T->Mi[lane][k] >= 0) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
+#pragma unroll
+          for (int k = 0; k < 12; ++k) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
           QV[12 * i + lane] -= acc;
         }
         __syncthreads();
@@ -554,30 +560,34 @@ struct SolverCtx {
       if (lane < 12) {
         const double* Di = DV + 78 * i;
         double acc = 0.0;
+#pragma unroll
         for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * QV[12 * i + k];
         WV[12 * i + lane] = acc;
       }
       __syncthreads();
     }
+    PROF_ADD_CTX((*this), 4);
     // backward: y_{N-1} = w_{N-1} ; y_i = w_i - D_i^-1 S_{i+1,i}^T y_{i+1}   (y stored in QV)
     if (lane < 12) QV[12 * (N - 1) + lane] = WV[12 * (N - 1) + lane];
     __syncthreads();
     for (int i = N - 2; i >= 0; --i) {
       if (lane < 12) {
         double acc = 0.0;
-        for (int r = 0; r < 12; ++r)
-          if (T->Mi[r][lane] >= 0) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
         SC[lane] = acc;
       }
       __syncthreads();
       if (lane < 12) {
         const double* Di = DV + 78 * i;
         double acc = 0.0;
+#pragma unroll
         for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * SC[k];
         QV[12 * i + lane] = WV[12 * i + lane] - acc;
       }
       __syncthreads();
     }
+    PROF_ADD_CTX((*this), 5);
     // dx = t - Phi^-1 A_dyn^T dy ; x-moment duals from the exact 2x2 elimination
     for (int c = lane; c < 12 * N; c += 64) {
       const int k = c / 12 + 1, j = c % 12;
@@ -644,6 +654,7 @@ struct SolverCtx {
       DS[q] = -RS[q] - gd + kDelta * dz;
     }
     __syncthreads();
+    PROF_ADD_CTX((*this), 6);
   }
 
   // kRefineSteps refinement steps (pdipm_srbd.hpp FastCtx::refine: later steps restore the original
@@ -767,9 +778,11 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
   bool floor_hit = false;
+  PROF_MARK_CTX(C);
   for (int it = 0; it < args.n_iter; ++it) {
     double mu;
     SRBD_GCALL(mu = C.residuals());
+    PROF_ADD_CTX(C, 0);
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
       double a = 0.0, b = 0.0, c = 0.0;
       for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
@@ -786,6 +799,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     SRBD_GCALL(C.solve());
     SRBD_GCALL(C.template refine<kInl>());  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
     SRBD_GCALL(C.residuals());  // restores RX, RS, RE for the combined solve
+    PROF_ADD_CTX(C, 0);
     double ap, ad;
     SRBD_GCALL(ap = C.step_length(C.S, C.DS));
     SRBD_GCALL(ad = C.step_length(C.Z, C.DZ));
@@ -819,7 +833,9 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
     mu_new = wave_sum(szn) / m;
     __syncthreads();
+    PROF_ADD_CTX(C, 8);
   }
+  PROF_FLUSH(C);
   double* xo = solver_out(args, 0) + (size_t)env * nz;
   double* so = solver_out(args, 1) + (size_t)env * m;
   double* zo = solver_out(args, 2) + (size_t)env * m;
