@@ -71,6 +71,8 @@ __device__ inline double* solver_out(const SolverArgs& a, int i) {
 }
 
 constexpr int kTablesDoubles = (int)((sizeof(Tables) + 15) / 16) * 2;
+// the same tables as a compile-time constant: lookups at indices known after unrolling fold away
+constexpr Tables kTabs = make_tables();
 
 // LDS carve (doubles) for horizon N; every offset is a multiple of 2 doubles (16 B).
 struct SolverLayout {
@@ -171,8 +173,42 @@ struct SolverCtx {
     const int o = T->Ni[r][j];
     return o >= 0 ? AV[a_ublock(N, i) + o] : 0.0;
   }
-  __device__ double E6(int i) const { return AV[a_ublock(N, i) + T->e6]; }
-  __device__ double E9(int i) const { return AV[a_ublock(N, i) + T->e9]; }
+  __device__ double E6(int i) const { return AV[a_ublock(N, i) + kTabs.e6]; }
+  __device__ double E9(int i) const { return AV[a_ublock(N, i) + kTabs.e9]; }
+  // f(q, k) for the G entries of u column j (CCS value q, stage-local row k) in CCS order: the 28
+  // candidate entries unrolled against the compile-time tables (no table loads; the same summation
+  // order as the loop over the column's entries)
+  // acc += sum over the G entries of u column j of stage i (CCS order) of value * v[stage-local row].
+  // kFast (the general kernel, everything inlined): the 28 candidates unrolled against the
+  // compile-time tables; otherwise (the fallback's out-of-line phases, whose register use the calling
+  // stage-invariant kernel has to save around the call) the plain loop over the tables.
+  template <bool kFast>
+  __device__ void gcol_dot(int i, int j, const double* v, double& acc) const {
+    if constexpr (kFast) {
+#pragma unroll
+      for (int q = 0; q < 28; ++q)
+        if (kTabs.gcol[q] == j) acc += G(i, q) * v[kTabs.grow[q]];
+    } else {
+      for (int q = 0; q < 28; ++q)
+        if (T->gcol[q] == j) acc += G(i, q) * v[T->grow[q]];
+    }
+  }
+  // s + sum_t AV[b + t] * v[idx[t]] over the n <= NMAX entries of a CCS column, added in order
+  // (kFast: unrolled, clamped indices, no branch)
+  template <bool kFast, int NMAX>
+  __device__ double col_dot(int b, int n, const int8_t* idx, const double* v, double s) const {
+    if constexpr (kFast) {
+#pragma unroll
+      for (int t = 0; t < NMAX; ++t) {
+        const int tt = t < n ? t : 0;
+        const double p_ = AV[b + tt] * v[idx[tt]];
+        s += t < n ? p_ : 0.0;
+      }
+    } else {
+      for (int t = 0; t < n; ++t) s += AV[b + t] * v[idx[t]];
+    }
+    return s;
+  }
   __device__ double phix(int k, int j) const { return HV[12 * (k - 1) + j] + kBeta; }  // x_k, k >= 1
   __device__ double phiu(int i, int j) const { return HV[12 * N + 12 * i + j] + kBeta; }
   // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i), precomputed
@@ -215,17 +251,17 @@ struct SolverCtx {
 
   // ---------------------------------------------------------------------- residuals ----
   // rx = Qx + f + G^T z + A^T y ; re = A x - b ; rs = G x + s - h ; returns mu = s'z/m
+  template <bool kFast = false>
   __device__ double residuals() {
     for (int c = lane; c < nz; c += 64) {
       double v = HV[c] * X[c] + fg[c];
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
-        for (int q = 0; q < 28; ++q)
-          if (T->gcol[q] == j) gz += G(i, q) * Z[16 * i + T->grow[q]];
+        gcol_dot<kFast>(i, j, Z + 16 * i, gz);
         double ay = 0.0;
         const int ub = a_ublock(N, i) + T->cpu[j];
-        for (int t = 0; t < T->su_n[j]; ++t) ay += AV[ub + t] * Y[12 * i + T->su[j][t]];
+        ay = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], Y + 12 * i, ay);
         if (j == 6) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i];
         if (j == 9) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
@@ -235,7 +271,7 @@ struct SolverCtx {
         if (k < N) {
           const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * Y[12 * (k - 1) + j];
-          for (int t = 0; t < T->sx_n[j]; ++t) ay += AV[xb + 1 + t] * Y[12 * k + T->sx[j][t]];
+          ay = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], Y + 12 * k, ay);
         } else {
           ay = AV[36 * (N - 1) + j] * Y[12 * (k - 1) + j];
         }
@@ -424,6 +460,7 @@ struct SolverCtx {
   // RX <- -(e1 - G^T q) (G^T over the updated DZ), RE <- -e4; dx and dy saved to the output rows for
   // solve(true). RX, RE, RS are overwritten (the caller restores them with residuals() after
   // refining the affine direction).
+  template <bool kFast = false>
   __device__ void refine_rhs() {
     for (int q = lane; q < m; q += 64) {  // step 0 (rows 2 and 3)
       const int i = q / 16, k = q % 16;
@@ -445,11 +482,10 @@ struct SolverCtx {
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
-        for (int q = 0; q < 28; ++q)
-          if (T->gcol[q] == j) gz += G(i, q) * DZ[16 * i + T->grow[q]];
+        gcol_dot<kFast>(i, j, DZ + 16 * i, gz);
         double ay = 0.0;
         const int ub = a_ublock(N, i) + T->cpu[j];
-        for (int t = 0; t < T->su_n[j]; ++t) ay += AV[ub + t] * DY[12 * i + T->su[j][t]];
+        ay = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], DY + 12 * i, ay);
         if (j == 6) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i];
         if (j == 9) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
@@ -459,7 +495,7 @@ struct SolverCtx {
         if (k < N) {
           const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * DY[12 * (k - 1) + j];
-          for (int t = 0; t < T->sx_n[j]; ++t) ay += AV[xb + 1 + t] * DY[12 * k + T->sx[j][t]];
+          ay = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], DY + 12 * k, ay);
         } else {
           ay = AV[36 * (N - 1) + j] * DY[12 * (k - 1) + j];
         }
@@ -490,6 +526,7 @@ struct SolverCtx {
   // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV, RS from refine_rhs's
   // step 0 carry rows 2 and 3), then dx = saved + correction before dz, ds are formed; DY is the
   // correction.
+  template <bool kFast = false>
   __device__ void solve(bool ref = false) {
     if (!ref)
       for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
@@ -500,8 +537,7 @@ struct SolverCtx {
       if (c >= 12 * N && !ref) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double g = 0.0;
-        for (int q = 0; q < 28; ++q)
-          if (T->gcol[q] == j) g += G(i, q) * VV[16 * i + T->grow[q]];
+        gcol_dot<kFast>(i, j, VV + 16 * i, g);
         v -= g;
       }
       R1T[c] = v;
@@ -595,7 +631,7 @@ struct SolverCtx {
       if (k < N) {
         const int xb = a_xblock(k) + T->cpx[j];
         aty = AV[xb] * QV[12 * (k - 1) + j];
-        for (int t = 0; t < T->sx_n[j]; ++t) aty += AV[xb + 1 + t] * QV[12 * k + T->sx[j][t]];
+        aty = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], QV + 12 * k, aty);
       } else {
         aty = AV[36 * (N - 1) + j] * QV[12 * (k - 1) + j];
       }
@@ -609,7 +645,7 @@ struct SolverCtx {
       auto aty_u = [&](int j) {
         const int ub = a_ublock(N, i) + T->cpu[j];
         double a = 0.0;
-        for (int t = 0; t < T->su_n[j]; ++t) a += AV[ub + t] * QV[12 * i + T->su[j][t]];
+        a = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], QV + 12 * i, a);
         return a;
       };
       if (foot) {
@@ -664,10 +700,10 @@ struct SolverCtx {
     for (int step = 0; step < kRefineSteps; ++step) {
       if (step > 0) {
         for (int e = lane; e < p; e += 64) DY[e] = ysg[e] + DY[e];
-        SRBD_GCALL(residuals());
+        SRBD_GCALL(this->template residuals<kInl>());
       }
-      SRBD_GCALL(refine_rhs());
-      SRBD_GCALL(solve(true));
+      SRBD_GCALL(this->template refine_rhs<kInl>());
+      SRBD_GCALL(this->template solve<kInl>(true));
     }
   }
 
@@ -781,7 +817,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   PROF_MARK_CTX(C);
   for (int it = 0; it < args.n_iter; ++it) {
     double mu;
-    SRBD_GCALL(mu = C.residuals());
+    SRBD_GCALL(mu = C.template residuals<kInl>());
     PROF_ADD_CTX(C, 0);
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
       double a = 0.0, b = 0.0, c = 0.0;
@@ -796,9 +832,9 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
-    SRBD_GCALL(C.solve());
+    SRBD_GCALL(C.template solve<kInl>());
     SRBD_GCALL(C.template refine<kInl>());  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
-    SRBD_GCALL(C.residuals());  // restores RX, RS, RE for the combined solve
+    SRBD_GCALL(C.template residuals<kInl>());  // restores RX, RS, RE for the combined solve
     PROF_ADD_CTX(C, 0);
     double ap, ad;
     SRBD_GCALL(ap = C.step_length(C.S, C.DS));
@@ -814,7 +850,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q])) + -(C.SI[q] * rc);
     }
     __syncthreads();
-    SRBD_GCALL(C.solve());
+    SRBD_GCALL(C.template solve<kInl>());
     SRBD_GCALL(C.template refine<kInl>());
     double apc, adc;
     SRBD_GCALL(apc = C.step_length(C.S, C.DS));
