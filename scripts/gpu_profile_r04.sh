@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04p
 mkdir -p $O
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --kernel-reps 2"
+B20="python3 bench.py --horizon 20 --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --kernel-reps 2"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && \
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $O/bench_driver_form.json 2> $O/bench_driver_form.err && \
@@ -17,7 +18,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-for
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B > $O/pmc2.json 2> $O/pmc2.err && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES -d $O/pmc_sq -o run --output-format csv -- $B > $O/pmc_sq.json 2> $O/pmc_sq.err && \
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH -d $O/pmc_sq2 -o run --output-format csv -- $B > $O/pmc_sq2.json 2> $O/pmc_sq2.err && \
-B20="python3 bench.py --horizon 20 --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --kernel-reps 2"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES -d $O/pmc_sq20 -o run --output-format csv -- $B20 > $O/pmc_sq20.json 2> $O/pmc_sq20.err && \
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH -d $O/pmc_sq20b -o run --output-format csv -- $B20 > $O/pmc_sq20b.json 2> $O/pmc_sq20b.err && \
 timeout -k 10 900 python3 -u scripts/bench_configs.py $O/configs.json > $O/configs.log 2>&1 && \
