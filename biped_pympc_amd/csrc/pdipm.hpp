@@ -26,6 +26,7 @@
 // diagonal dual blocks) is spread over the 64 lanes; the stage recursion is sequential.
 #pragma once
 #include "srbd_common.hpp"
+#include "dpp_rows.hpp"
 
 namespace srbd {
 
@@ -74,10 +75,24 @@ constexpr int kTablesDoubles = (int)((sizeof(Tables) + 15) / 16) * 2;
 // the same tables as a compile-time constant: lookups at indices known after unrolling fold away
 constexpr Tables kTabs = make_tables();
 
+// The dual coupling S_{i,i-1} = M_i diag(P_{i-1} / phi_x(x_i)) has M_i's CCS pattern, which the twisted
+// chains of SolverCtx (as those of pdipm_srbd.hpp FastCtx) rely on: row c holds {c}, plus {6, 7, 8}
+// for c < 3 and {c + 6} for 3 <= c < 6; and pi C^T pi^T (pi = perm12) has the same pattern, so the
+// backward group runs the forward group's instructions.
+constexpr bool coupling_pattern_ok() {
+  for (int r = 0; r < 12; ++r)
+    for (int j = 0; j < 12; ++j) {
+      const bool want = j == r || (r < 3 && j >= 6 && j <= 8) || (r >= 3 && r < 6 && j == r + 6);
+      if ((kTabs.Mi[r][j] >= 0) != want || (kTabs.Mi[perm12(j)][perm12(r)] >= 0) != want) return false;
+    }
+  return true;
+}
+static_assert(coupling_pattern_ok(), "A's x-block pattern is not the one the twisted chains assume");
+
 // LDS carve (doubles) for horizon N; every offset is a multiple of 2 doubles (16 B).
 struct SolverLayout {
   int AV, GV, HV, X, S, Z, Y, RX, RS, RE, SI, WD, DI, R2, VV, PH, DV, R1T, TV, QV, WV, DS, DZ, DY, SC,
-      TB, CV, total;
+      TB, CV, KX, total;
   __host__ __device__ SolverLayout(int N) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
     int o = 0;
@@ -90,11 +105,13 @@ struct SolverLayout {
     R1T = take(nz); TV = take(nz);
     QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
-    SC = take(160);
+    SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector (the twisted chains)
     TB = take(kTablesDoubles);  // a copy of c_tab: the index tables, read with lane-varying indices
     // the dual couplings S_{i,i-1} over x_i's 36-value block (Ssub), where they still fit the 160 KiB
     // of LDS a workgroup may have (all horizons but 32; without them Ssub is formed on the fly)
     CV = (o + 36 * N) * 8 <= 160 * 1024 ? take(36 * N) : -1;
+    // the constant x part of every S_ii (sii_x; the general kernel only), where it still fits
+    KX = (CV >= 0 && (o + 78 * N) * 8 <= 160 * 1024) ? take(78 * N) : -1;
     total = o;
   }
 };
@@ -160,6 +177,7 @@ struct SolverCtx {
   // the index tables (a copy of c_tab in LDS where one fits: its lookups take lane-varying indices,
   // which from constant memory are vector loads of L2 latency on every chain step) and the couplings
   double* CV;
+  double* KX;  // sii_x of every stage (packed lower, 78 per stage), or null: formed in factor()
   const Tables* T;
   PROF_DECL  // diagnostic phase stamps (scripts/general_phase_profile.py); empty in the product build
 
@@ -239,15 +257,59 @@ struct SolverCtx {
     }
     return s;
   }
-  // CV: the QP's constant couplings (H and A do not change across the Newton iterations)
+  // The x part of S_ii (entry (r, c), r >= c): P_i^2 / phi_x(x_{i+1}) + delta on the diagonal plus
+  // sum_j M_i[r][j] M_i[c][j] / phi_x(x_i)[j] -- constant over the Newton iterations
+  __device__ double sii_x(int i, int r, int c) const {
+    double v = 0.0;
+    if (r == c) {
+      const double pr = Pv(i, r);
+      v = pr * pr / phix(i + 1, r) + kDelta;
+    }
+    if (i >= 1)
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const int o1 = T->Mi[r][j], o2 = T->Mi[c][j];
+        const bool nz = o1 >= 0 && o2 >= 0;
+        const double t = AV[a_xblock(i) + (nz ? o1 : 0)] * AV[a_xblock(i) + (nz ? o2 : 0)] / phix(i, j);
+        v += nz ? t : 0.0;
+      }
+    return v;
+  }
+  // CV / KX: the QP's constant couplings and S_ii x parts (H and A do not change across the Newton
+  // iterations); kK: KX is in use (the general kernel)
+  template <bool kK>
   __device__ void couplings() {
-    if (!CV) return;
-    for (int e = lane; e < 36 * (N - 1); e += 64) {
-      const int i = e / 36 + 1, o = e % 36, j = T->xb_j[o];
-      CV[e] = T->xb_r[o] >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, j) / phix(i, j) : 0.0;
+    if (CV)
+      for (int e = lane; e < 36 * (N - 1); e += 64) {
+        const int i = e / 36 + 1, o = e % 36, j = T->xb_j[o];
+        CV[e] = T->xb_r[o] >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, j) / phix(i, j) : 0.0;
+      }
+    if constexpr (kK) {
+      if (KX)
+        for (int e = lane; e < 78 * N; e += 64) {
+          const int i = e / 78, l = e % 78;
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= l) ++r;
+          KX[e] = sii_x(i, r, l - r * (r + 1) / 2);
+        }
     }
   }
   __device__ double G(int i, int q) const { return GV[28 * i + q]; }
+  // S_{i,i-1} at x_i's CCS offset o (CV, or formed on the fly where CV did not fit)
+  __device__ double cpl(int i, int o) const {
+    if (CV) return CV[a_xblock(i) + o];
+    const int j = T->xb_j[o];
+    return AV[a_xblock(i) + o] * Pv(i - 1, j) / phix(i, j);
+  }
+  // Entry (c, b) of the coupling seen by twisted group g (pdipm_srbd.hpp FastCtx::cg, per stage):
+  // C = S_{i,i-1} (g = 0) or pi C^T pi^T (g = 1). cg_off: its offset inside the x block (-1: a
+  // structural zero), runtime indices from the LDS table; cgk: the value at compile-time c, b (after
+  // unrolling both candidate offsets fold), `stage` the i of the S_{i,i-1} it comes from.
+  __device__ int cg_off(int g, int c, int b) const { return g ? T->Mi[perm12(b)][perm12(c)] : T->Mi[c][b]; }
+  __device__ double cgk(int g, int stage, int c, int b) const {
+    return cpl(stage, g ? kTabs.Mi[perm12(b)][perm12(c)] : kTabs.Mi[c][b]);
+  }
+  __device__ double cg_at(int stage, int o) const { return o >= 0 ? cpl(stage, o) : 0.0; }
 
   // ---------------------------------------------------------------------- residuals ----
   // rx = Qx + f + G^T z + A^T y ; re = A x - b ; rs = G x + s - h ; returns mu = s'z/m
@@ -306,6 +368,7 @@ struct SolverCtx {
   }
 
   // ---------------------------------------------------------------------- factorise ----
+  template <bool kFast = false>
   __device__ void factor() {
     for (int q = lane; q < m; q += 64) {
       const double si = 1.0 / S[q];
@@ -360,19 +423,9 @@ struct SolverCtx {
       int r = 0;
       while ((r + 1) * (r + 2) / 2 <= l) ++r;
       const int c = l - r * (r + 1) / 2;
-      double v = 0.0;
-      if (r == c) {
-        const double pr = Pv(i, r);
-        v = pr * pr / phix(i + 1, r) + kDelta;
-      }
-      if (i >= 1)
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          const int o1 = T->Mi[r][j], o2 = T->Mi[c][j];
-          const bool nz = o1 >= 0 && o2 >= 0;
-          const double t = AV[a_xblock(i) + (nz ? o1 : 0)] * AV[a_xblock(i) + (nz ? o2 : 0)] / phix(i, j);
-          v += nz ? t : 0.0;
-        }
+      double v;
+      if constexpr (kFast) v = KX ? KX[e] : sii_x(i, r, c);
+      else v = sii_x(i, r, c);
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         double vr[4], vc[4];
@@ -396,6 +449,109 @@ struct SolverCtx {
     }
     __syncthreads();
     PROF_ADD_CTX((*this), 1);
+    if constexpr (kFast) {
+    // Twisted block recursion (pdipm_srbd.hpp FastCtx::factor with the couplings of each stage),
+    // register-resident, one block row per lane, no workgroup barrier inside:
+    //   group 0 (lanes 0..15)  forward  D_i = S_ii - C_i D_{i-1}^-1 C_i^T                 i = 0 .. mid-1
+    //   group 1 (lanes 16..31) backward E_j = S_jj - C_{j+1}^T E_{j+1}^-1 C_{j+1}         j = N-1 .. mid+1
+    //   middle (group 0)       T = S_mm - C_m D_{m-1}^-1 C_m^T - C_{m+1}^T E_{m+1}^-1 C_{m+1}
+    // with C_i = S_{i,i-1}; group 1 in pi-permuted coordinates. Each 12x12 block is inverted in
+    // registers (inverse_rows12) and stored, original coordinates packed lower, in DV: D_i^-1 (i < mid),
+    // T^-1 (mid), E_j^-1 (j > mid). Half the sequential steps of the one-sided recursion.
+    {
+      const int mid = N / 2, nf = mid, nb = N - 1 - mid;
+      const int TT = nf > nb ? nf : nb;
+      if (lane < 32) {
+        const int g = lane >> 4;
+        const int r = (lane & 15) < 12 ? (lane & 15) : 11;
+        const bool own = (lane & 15) < 12;
+        const int pr = g ? perm12(r) : r;
+        const int cnt = g ? nb : nf;
+        double* Vs = SC + 144 * g;  // per-group scratch for V = D^-1 Cg^T
+        double* XB = SC + 288;      // group 1's C^T E^-1 C (permuted) for the middle block
+        // offsets of row r's coupling entries: (r, r), (r, 6..8) for r < 3, (r, r + 6) for 3 <= r < 6
+        const int oRR = cg_off(g, r, r);
+        const int o6 = r < 3 ? cg_off(g, r, 6) : 0, o7 = r < 3 ? cg_off(g, r, 7) : 0;
+        const int o8 = r < 3 ? cg_off(g, r, 8) : 0, oR6 = (r >= 3 && r < 6) ? cg_off(g, r, r + 6) : 0;
+        double Dr[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) Dr[c] = 0.0;
+#pragma unroll 1
+        for (int t = 0; t <= TT; ++t) {
+          const bool mstep = (t == TT);
+          const int i = mstep ? mid : (g ? N - 1 - t : t);
+          const bool act = mstep ? (g == 0 || nb >= 1) : (t < cnt);
+          const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+          const int cs = g ? i + 1 : i;  // the S_{cs,cs-1} this step applies
+          double Sr[12];
+          if (act) {
+            const double* Si = DV + 78 * i;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) Sr[c] = Si[sym_idx(pr, g ? perm12(c) : c)];
+            if (prev) {
+              double V[12];  // row r of D^-1 Cg^T
+#pragma unroll
+              for (int c = 0; c < 12; ++c) {
+                double v = Dr[c] * cgk(g, cs, c, c);
+                if (c < 3) v += Dr[6] * cgk(g, cs, c, 6) + Dr[7] * cgk(g, cs, c, 7) + Dr[8] * cgk(g, cs, c, 8);
+                else if (c < 6) v += Dr[c + 6] * cgk(g, cs, c, c + 6);
+                V[c] = v;
+              }
+              lds_wave_sync();
+              if (own) {
+#pragma unroll
+                for (int c = 0; c < 12; ++c) Vs[r * 12 + c] = V[c];
+              }
+              lds_wave_sync();
+              double X[12];  // row r of Cg V
+              const double cr = cpl(cs, oRR);
+#pragma unroll
+              for (int c = 0; c < 12; ++c) X[c] = cr * Vs[r * 12 + c];
+              if (r < 3) {
+                const double c6 = cpl(cs, o6), c7 = cpl(cs, o7), c8 = cpl(cs, o8);
+#pragma unroll
+                for (int c = 0; c < 12; ++c) X[c] += c6 * Vs[72 + c] + c7 * Vs[84 + c] + c8 * Vs[96 + c];
+              } else if (r < 6) {
+                const double c9 = cpl(cs, oR6);
+#pragma unroll
+                for (int c = 0; c < 12; ++c) X[c] += c9 * Vs[(r + 6) * 12 + c];
+              }
+              if (mstep && g == 1) {
+                if (own) {
+#pragma unroll
+                  for (int c = 0; c < 12; ++c) XB[r * 12 + c] = X[c];
+                }
+              } else {
+#pragma unroll
+                for (int c = 0; c < 12; ++c) Sr[c] -= X[c];
+              }
+            }
+          }
+          if (mstep) {
+            lds_wave_sync();
+            if (g == 0 && nb >= 1) {  // un-permute group 1's term: X_b[r][c] = XB[pi r][pi c]
+#pragma unroll
+              for (int c = 0; c < 12; ++c) Sr[c] -= XB[perm12(r) * 12 + perm12(c)];
+            }
+          }
+          if (act && !(mstep && g == 1)) {
+            inverse_rows12(Sr, Dr);
+            if (own) {
+              double* Di = DV + 78 * i;
+#pragma unroll
+              for (int c = 0; c < 12; ++c) {
+                const int pc = g ? perm12(c) : c;
+                if (pc <= pr) Di[pr * (pr + 1) / 2 + pc] = Dr[c];
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    } else {
+    // (the in-launch fallback, an out-of-line call from the stage-invariant kernels: the one-sided
+    // recursion, whose registers leave those kernels spill-free around the call)
     // block recursion over stages: D_i = S_ii - S_{i,i-1} D_{i-1}^-1 S_{i,i-1}^T ; DV_i <- D_i^-1
     for (int i = 0; i < N; ++i) {
       double* Di = DV + 78 * i;
@@ -450,6 +606,7 @@ struct SolverCtx {
       if (own0) Di[e0] = -Di[e0];
       if (e1 < 78) Di[e1] = -Di[e1];
       __syncthreads();
+    }
     }
     PROF_ADD_CTX((*this), 2);
   }
@@ -582,6 +739,112 @@ struct SolverCtx {
     }
     __syncthreads();
     PROF_ADD_CTX((*this), 3);
+    if constexpr (kFast) {
+    // Twisted block solve with the factors of factor() (pdipm_srbd.hpp FastCtx::solve, per-stage couplings):
+    //   elimination: group 0  q_i = g_i - C_i w_{i-1},         w_i = D_i^-1 q_i   (i = 0 .. mid-1)
+    //                group 1  p_j = g_j - C_{j+1}^T v_{j+1},   v_j = E_j^-1 p_j   (j = N-1 .. mid+1)
+    //   middle:      y_mid = T^-1 (g_mid - C_m w_{mid-1} - C_{m+1}^T v_{mid+1})
+    //   outward:     group 0  y_i = w_i - D_i^-1 C_{i+1}^T y_{i+1};  group 1  y_j = v_j - E_j^-1 C_j y_{j-1}
+    // g is read from QV, y written back to QV; w / v kept in WV. Crow / Ccol: row / column r of the
+    // coupling (zeros included), DPP-broadcast products over the 16-lane group.
+    {
+      const int mid = N / 2, nf = mid, nb = N - 1 - mid;
+      const int TT = nf > nb ? nf : nb;
+      if (lane < 32) {
+        const int g = lane >> 4;
+        const int r = (lane & 15) < 12 ? (lane & 15) : 11;
+        const bool own = (lane & 15) < 12;
+        const int pr = g ? perm12(r) : r;
+        const int cnt = g ? nb : nf;
+        int oRow[12], oCol[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+          oRow[j] = cg_off(g, r, j);
+          oCol[j] = cg_off(g, j, r);
+        }
+        double w = 0.0;
+#pragma unroll 1
+        for (int t = 0; t <= TT; ++t) {
+          const bool mstep = (t == TT);
+          const int i = mstep ? mid : (g ? N - 1 - t : t);
+          const bool act = mstep ? (g == 0 || nb >= 1) : (t < cnt);
+          const bool prev = mstep ? (cnt >= 1) : (t >= 1);
+          double cw = 0.0;  // Cg times the previous w (both groups)
+          if (act && prev) {
+            const int cs = g ? i + 1 : i;
+            double Crow[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) Crow[j] = cg_at(cs, oRow[j]);
+            double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              c0 += Crow[j] * bc16(w, j);
+              c1 += Crow[j + 4] * bc16(w, j + 4);
+              c2 += Crow[j + 8] * bc16(w, j + 8);
+            }
+            cw = (c0 + c1) + c2;
+          }
+          if (mstep) {  // group 1 hands C^T v_{mid+1} (original coordinates) to group 0
+            if (g == 1 && own && nb >= 1) SC[432 + pr] = cw;
+            lds_wave_sync();
+          }
+          if (act && !(mstep && g == 1)) {
+            const double* Di = DV + 78 * i;
+            double Dr[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12(k) : k)];
+            double q = QV[12 * i + pr] - cw;
+            if (mstep && nb >= 1) q -= SC[432 + r];
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              a0 += Dr[k] * bc16(q, k);
+              a1 += Dr[k + 4] * bc16(q, k + 4);
+              a2 += Dr[k + 8] * bc16(q, k + 8);
+            }
+            w = (a0 + a1) + a2;
+            if (own) WV[12 * i + pr] = w;
+          }
+        }
+        PROF_ADD_CTX((*this), 4);
+        // outward substitution from the middle block (y_mid = group 0's last w, also in WV_mid)
+        lds_wave_sync();
+        if (own && g == 0) QV[12 * mid + r] = w;
+        double y = (g == 0) ? w : WV[12 * mid + pr];
+#pragma unroll 1
+        for (int t = 0; t < TT; ++t) {
+          const int i = g ? mid + 1 + t : mid - 1 - t;
+          if (t < cnt) {
+            const int cs = g ? i : i + 1;
+            double Ccol[12], Dr[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) Ccol[j] = cg_at(cs, oCol[j]);
+            const double* Di = DV + 78 * i;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) Dr[k] = Di[sym_idx(pr, g ? perm12(k) : k)];
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // Cg^T y_prev
+              s0 += Ccol[j] * bc16(y, j);
+              s1 += Ccol[j + 4] * bc16(y, j + 4);
+              s2 += Ccol[j + 8] * bc16(y, j + 8);
+            }
+            const double sc = (s0 + s1) + s2;
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              a0 += Dr[k] * bc16(sc, k);
+              a1 += Dr[k + 4] * bc16(sc, k + 4);
+              a2 += Dr[k + 8] * bc16(sc, k + 8);
+            }
+            y = WV[12 * i + pr] - ((a0 + a1) + a2);
+            if (own) QV[12 * i + pr] = y;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    } else {
     // forward: q_i -= S_{i,i-1} w_{i-1} ; w_i = D_i^-1 q_i
     for (int i = 0; i < N; ++i) {
       if (i >= 1) {
@@ -622,6 +885,7 @@ struct SolverCtx {
         QV[12 * i + lane] = WV[12 * i + lane] - acc;
       }
       __syncthreads();
+    }
     }
     PROF_ADD_CTX((*this), 5);
     // dx = t - Phi^-1 A_dyn^T dy ; x-moment duals from the exact 2x2 elimination
@@ -767,7 +1031,10 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     }
     if (Lo.CV >= 0) place(C.CV, Lo.CV, 36 * N);
     else C.CV = nullptr;
-    place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 160); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
+    C.KX = nullptr;
+    if constexpr (kInl)
+      if (Lo.KX >= 0) place(C.KX, Lo.KX, 78 * N);
+    place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 448); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
     place(C.PH, Lo.PH, 24 * N); place(C.TV, Lo.TV, nz); place(C.R1T, Lo.R1T, nz);
     place(C.DI, Lo.DI, m); place(C.WD, Lo.WD, m); place(C.SI, Lo.SI, m); place(C.VV, Lo.VV, m);
     place(C.R2, Lo.R2, m); place(C.DS, Lo.DS, m); place(C.DZ, Lo.DZ, m); place(C.DY, Lo.DY, p);
@@ -809,7 +1076,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     for (int e = lane; e < p; e += 64) C.Y[e] = args.y0;
   }
   __syncthreads();
-  C.couplings();
+  C.template couplings<kInl>();
   __syncthreads();
 
   double res0 = 0.0, res1 = 0.0, res2 = 0.0, mu_new = 0.0;
@@ -828,7 +1095,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       res1 = sqrt(wave_sum(b));
       res2 = sqrt(wave_sum(c));
     }
-    SRBD_GCALL(C.factor());
+    SRBD_GCALL(C.template factor<kInl>());
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();

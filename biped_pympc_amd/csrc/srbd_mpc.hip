@@ -109,7 +109,10 @@ struct ScratchPool {
 // the precomputed couplings are dropped where they would not fit 160 KiB of LDS)
 int general_slot_doubles() {
   int s = 0;
-  for (int n = 1; n <= srbd::kMaxN; ++n) s = std::max(s, srbd::SolverLayout(n).total);
+  for (int n = 1; n <= srbd::kMaxN; ++n) {  // (KX, the last array, is the general kernel's only)
+    const srbd::SolverLayout L(n);
+    s = std::max(s, L.KX >= 0 ? L.KX : L.total);
+  }
   return s;
 }
 srbd::PerDevice<ScratchPool> g_scratch;

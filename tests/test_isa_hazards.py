@@ -1,6 +1,6 @@
 """Static audit of the DPP wait states in the product kernels (CPU only: hipcc cross-compiles).
 
-The broadcast-FMA asm blocks (csrc/pdipm_srbd.hpp SRBD_FMAC_BC) open with `s_nop 1` and carry no
+The broadcast-FMA asm blocks (csrc/dpp_rows.hpp SRBD_FMAC_BC) open with `s_nop 1` and carry no
 trailing wait states, and inside a block a DPP reads no VGPR written by either of the 2 instructions
 before it. A wrong wait state gives wrong values with no fault, and possibly only under some wave
 interleavings, so the final ISA of both translation units -- compiled with the product build's own
