@@ -107,8 +107,8 @@ struct SolverLayout {
     DS = take(m); DZ = take(m); DY = take(p);
     SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector (the twisted chains)
     TB = take(kTablesDoubles);  // a copy of c_tab: the index tables, read with lane-varying indices
-    // the dual couplings S_{i,i-1} over x_i's 36-value block (Ssub), where they still fit the 160 KiB
-    // of LDS a workgroup may have (all horizons but 32; without them Ssub is formed on the fly)
+    // the dual couplings S_{i,i-1} = M_i diag(P_{i-1} / phi_x(x_i)) over x_i's 36-value block (cpl), where
+    // they still fit the 160 KiB of LDS a workgroup may have (all horizons but 32; else formed on the fly)
     CV = (o + 36 * N) * 8 <= 160 * 1024 ? take(36 * N) : -1;
     // the constant x part of every S_ii (sii_x; the general kernel only), where it still fits
     KX = (CV >= 0 && (o + 78 * N) * 8 <= 160 * 1024) ? take(78 * N) : -1;
@@ -229,15 +229,6 @@ struct SolverCtx {
   }
   __device__ double phix(int k, int j) const { return HV[12 * (k - 1) + j] + kBeta; }  // x_k, k >= 1
   __device__ double phiu(int i, int j) const { return HV[12 * N + 12 * i + j] + kBeta; }
-  // S_{i,i-1}[r][c] = M_i[r][c] * P_{i-1}[c] / phi_x(x_i)[c]  (coupling through x_i), precomputed
-  // per QP into CV at the offsets of x_i's CCS block (couplings()): no division on the chains
-  // Branch-free (a structural zero reads an in-bounds value and returns 0): the callers' 12-term sums
-  // then issue their LDS loads together instead of one exec-masked round trip per term.
-  __device__ double Ssub(int i, int r, int c) const {
-    const int o = T->Mi[r][c], oc = o >= 0 ? o : 0;
-    const double v = CV ? CV[a_xblock(i) + oc] : AV[a_xblock(i) + oc] * Pv(i - 1, c) / phix(i, c);
-    return o >= 0 ? v : 0.0;
-  }
   // (M_i v)_r and (N_i v)_r of stage i (v: 12 entries), branch-free
   __device__ double mrow(int i, int r, const double* v) const {
     double s = 0.0;
@@ -449,7 +440,6 @@ struct SolverCtx {
     }
     __syncthreads();
     PROF_ADD_CTX((*this), 1);
-    if constexpr (kFast) {
     // Twisted block recursion (pdipm_srbd.hpp FastCtx::factor with the couplings of each stage),
     // register-resident, one block row per lane, no workgroup barrier inside:
     //   group 0 (lanes 0..15)  forward  D_i = S_ii - C_i D_{i-1}^-1 C_i^T                 i = 0 .. mid-1
@@ -549,65 +539,6 @@ struct SolverCtx {
       }
     }
     __syncthreads();
-    } else {
-    // (the in-launch fallback, an out-of-line call from the stage-invariant kernels: the one-sided
-    // recursion, whose registers leave those kernels spill-free around the call)
-    // block recursion over stages: D_i = S_ii - S_{i,i-1} D_{i-1}^-1 S_{i,i-1}^T ; DV_i <- D_i^-1
-    for (int i = 0; i < N; ++i) {
-      double* Di = DV + 78 * i;
-      if (i >= 1) {
-        const double* Dp = DV + 78 * (i - 1);
-        for (int e = lane; e < 144; e += 64) {
-          const int r = e / 12, c = e % 12;
-          double u = 0.0;
-#pragma unroll
-          for (int k = 0; k < 12; ++k) u += Ssub(i, r, k) * Dp[sym_idx(k, c)];
-          SC[e] = u;
-        }
-        __syncthreads();
-        for (int e = lane; e < 78; e += 64) {
-          int r = 0;
-          while ((r + 1) * (r + 2) / 2 <= e) ++r;
-          const int c = e - r * (r + 1) / 2;
-          double acc = 0.0;
-#pragma unroll
-          for (int k = 0; k < 12; ++k) acc += SC[r * 12 + k] * Ssub(i, c, k);
-          Di[e] -= acc;
-        }
-        __syncthreads();
-      }
-      // in-place symmetric sweep of the 12x12 block (78 packed entries over 64 lanes)
-      int r0 = 0, r1 = 0;
-      const int e0 = lane < 64 ? lane : 0, e1 = lane + 64;  // (an idle lane, lane >= 64, stores nothing)
-      while ((r0 + 1) * (r0 + 2) / 2 <= e0) ++r0;
-      if (e1 < 78)
-        while ((r1 + 1) * (r1 + 2) / 2 <= e1) ++r1;
-      const int c0 = e0 - r0 * (r0 + 1) / 2, c1 = e1 - r1 * (r1 + 1) / 2;
-      const bool own0 = lane < 64;
-      for (int k = 0; k < 12; ++k) {
-        const double id = 1.0 / Di[k * (k + 1) / 2 + k];
-        const double a0 = Di[e0], k0r = Di[sym_idx(r0, k)], k0c = Di[sym_idx(c0, k)];
-        double a1 = 0.0, k1r = 0.0, k1c = 0.0;
-        if (e1 < 78) { a1 = Di[e1]; k1r = Di[sym_idx(r1, k)]; k1c = Di[sym_idx(c1, k)]; }
-        __syncthreads();
-        double n0, n1 = 0.0;
-        if (r0 != k && c0 != k) n0 = a0 - k0r * k0c * id;
-        else if (r0 == k && c0 == k) n0 = -id;
-        else n0 = a0 * id;
-        if (e1 < 78) {
-          if (r1 != k && c1 != k) n1 = a1 - k1r * k1c * id;
-          else if (r1 == k && c1 == k) n1 = -id;
-          else n1 = a1 * id;
-        }
-        if (own0) Di[e0] = n0;
-        if (e1 < 78) Di[e1] = n1;
-        __syncthreads();
-      }
-      if (own0) Di[e0] = -Di[e0];
-      if (e1 < 78) Di[e1] = -Di[e1];
-      __syncthreads();
-    }
-    }
     PROF_ADD_CTX((*this), 2);
   }
 
@@ -739,7 +670,6 @@ struct SolverCtx {
     }
     __syncthreads();
     PROF_ADD_CTX((*this), 3);
-    if constexpr (kFast) {
     // Twisted block solve with the factors of factor() (pdipm_srbd.hpp FastCtx::solve, per-stage couplings):
     //   elimination: group 0  q_i = g_i - C_i w_{i-1},         w_i = D_i^-1 q_i   (i = 0 .. mid-1)
     //                group 1  p_j = g_j - C_{j+1}^T v_{j+1},   v_j = E_j^-1 p_j   (j = N-1 .. mid+1)
@@ -844,49 +774,6 @@ struct SolverCtx {
       }
     }
     __syncthreads();
-    } else {
-    // forward: q_i -= S_{i,i-1} w_{i-1} ; w_i = D_i^-1 q_i
-    for (int i = 0; i < N; ++i) {
-      if (i >= 1) {
-        if (lane < 12) {
-          double acc = 0.0;
-#pragma unroll
-          for (int k = 0; k < 12; ++k) acc += Ssub(i, lane, k) * WV[12 * (i - 1) + k];
-          QV[12 * i + lane] -= acc;
-        }
-        __syncthreads();
-      }
-      if (lane < 12) {
-        const double* Di = DV + 78 * i;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * QV[12 * i + k];
-        WV[12 * i + lane] = acc;
-      }
-      __syncthreads();
-    }
-    PROF_ADD_CTX((*this), 4);
-    // backward: y_{N-1} = w_{N-1} ; y_i = w_i - D_i^-1 S_{i+1,i}^T y_{i+1}   (y stored in QV)
-    if (lane < 12) QV[12 * (N - 1) + lane] = WV[12 * (N - 1) + lane];
-    __syncthreads();
-    for (int i = N - 2; i >= 0; --i) {
-      if (lane < 12) {
-        double acc = 0.0;
-#pragma unroll
-        for (int r = 0; r < 12; ++r) acc += Ssub(i + 1, r, lane) * QV[12 * (i + 1) + r];
-        SC[lane] = acc;
-      }
-      __syncthreads();
-      if (lane < 12) {
-        const double* Di = DV + 78 * i;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) acc += Di[sym_idx(lane, k)] * SC[k];
-        QV[12 * i + lane] = WV[12 * i + lane] - acc;
-      }
-      __syncthreads();
-    }
-    }
     PROF_ADD_CTX((*this), 5);
     // dx = t - Phi^-1 A_dyn^T dy ; x-moment duals from the exact 2x2 elimination
     for (int c = lane; c < 12 * N; c += 64) {

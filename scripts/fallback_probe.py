@@ -34,7 +34,7 @@ def qp_batch(B, N, flag_every, seed=77):
     return [H, G, A, f, d, b], [x, s, z, y]
 
 
-def timed(fn, reps=3):
+def timed(fn, reps=10):
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -9,7 +9,7 @@ mkdir -p gpurun_out/r04
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r04/pytest_gpu.txt 2>&1 || { tail -40 gpurun_out/r04/pytest_gpu.txt; exit 1; }
 tail -1 gpurun_out/r04/pytest_gpu.txt
 for v in ${PROBE_LIBS:-new slots old}; do
-  case $v in new) lib=;; slots) lib=ab/libsrbd_mpc_slots.so;; old) lib=ab/libsrbd_mpc_old.so;; esac
+  case $v in new) lib=;; slots) lib=ab/libsrbd_mpc_slots.so;; old) lib=ab/libsrbd_mpc_old.so;; prev) lib=ab/libsrbd_mpc_prev.so;; esac
   [ -z "$lib" ] || [ -f "$lib" ] || continue
   SRBD_LIB=$lib timeout -k 10 400 python scripts/fallback_probe.py > gpurun_out/r04/fallback_probe_$v.json 2> gpurun_out/r04/fallback_probe_$v.err || { tail -20 gpurun_out/r04/fallback_probe_$v.err; exit 1; }
   echo "$v $(cat gpurun_out/r04/fallback_probe_$v.json)"

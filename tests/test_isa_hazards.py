@@ -53,16 +53,23 @@ def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
     """Also, on the same ISA: the register kernels keep every VGPR in registers -- the fused step
     kernel (mpc_step_reg_kernel) at every horizon up to 24 and the CCS solver kernel
     (pdipm_srbd_reg_kernel, the CusADi drop-in's path) up to 20 (the three-wave QPs beyond spill a few
-    VGPRs)."""
+    VGPRs). The fused kernel has no spill at all; the CCS kernel's only ones are the
+    whole-wave save of its SGPR-spill register around the call of the in-launch general fallback
+    (pdipm.hpp pdipm_general_scratch), which runs for QPs that are not stage-invariant only: no spill
+    or reload instruction elsewhere, and at most 2 such registers."""
     from dpp_hazard_check import check
-    from kernel_resources import resources
+    from kernel_resources import body_spills, resources
     for s in _isa(tmp_path, unit):
         assert check(s) == 0, s
         for name, r in resources(s, "reg_kernel").items():
             n = _reg_horizon(name)
             limit = 24 if "mpc_step" in name else 20
             if n is not None and n <= limit:
-                assert r["vgpr_spill_count"] == 0, (name, r)
+                if "mpc_step" in name:
+                    assert r["vgpr_spill_count"] == 0, (name, r)
+                else:
+                    assert r["vgpr_spill_count"] <= 2, (name, r)
+                    assert body_spills(s, name) == [], (name, body_spills(s, name))
 
 
 def test_checker_detects_planted_hazards(tmp_path):
