@@ -63,6 +63,11 @@ __device__ __forceinline__ bool not_finite(double v) { return !__builtin_isfinit
 // kernels' one step sits at the FP64 floor at N = 10 / 20)
 constexpr int kRefineSteps = 1;
 
+// threads per QP in the general kernel (pdipm_kernel): two waves share its row-parallel loops (the
+// chains run on the first wave's 32 lanes); at ~410 VGPRs each wave has a SIMD to itself, and the two
+// QPs per CU its LDS allows at N = 10 then use all four SIMDs
+constexpr int kGeneralThreads = 128;
+
 
 __device__ inline const double* solver_in(const SolverArgs& a, int i) {
   return a.dev_in ? a.dev_in[i] : a.in[i];
@@ -92,7 +97,7 @@ static_assert(coupling_pattern_ok(), "A's x-block pattern is not the one the twi
 // LDS carve (doubles) for horizon N; every offset is a multiple of 2 doubles (16 B).
 struct SolverLayout {
   int AV, GV, HV, X, S, Z, Y, RX, RS, RE, SI, WD, DI, R2, VV, PH, DV, R1T, TV, QV, WV, DS, DZ, DY, SC,
-      TB, CV, KX, total;
+      RD, TB, CV, KX, total;
   __host__ __device__ SolverLayout(int N) {
     const int nz = 24 * N, m = 16 * N, p = 14 * N, nd = 12 * N;
     int o = 0;
@@ -106,6 +111,7 @@ struct SolverLayout {
     QV = take(nd); WV = take(nd);
     DS = take(m); DZ = take(m); DY = take(p);
     SC = take(448);  // 2 x 144 V scratch + 144 middle block + 12 middle vector (the twisted chains)
+    RD = take(8);    // the team reductions' wave partials
     TB = take(kTablesDoubles);  // a copy of c_tab: the index tables, read with lane-varying indices
     // the dual couplings S_{i,i-1} = M_i diag(P_{i-1} / phi_x(x_i)) over x_i's 36-value block (cpl), where
     // they still fit the 160 KiB of LDS a workgroup may have (all horizons but 32; else formed on the fly)
@@ -170,6 +176,10 @@ __device__ inline double ccs_gx(const double* Gv, int q, const double* xu) {
 
 struct SolverCtx {
   int N, nz, m, p, nd, lane;
+  // nt: the threads a QP's row-parallel loops stride over (kGeneralThreads in the general kernel; 64
+  // in the fallback, whose other waves are idle lanes); RD: one reduction partial per wave (LDS)
+  int nt;
+  double* RD;
   double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,
       *QV, *WV, *DS, *DZ, *DY, *SC;
   const double *fg, *hg, *bg;
@@ -210,6 +220,23 @@ struct SolverCtx {
       for (int q = 0; q < 28; ++q)
         if (T->gcol[q] == j) acc += G(i, q) * v[T->grow[q]];
     }
+  }
+  // s + (G_i xu)_k over inequality row k's entries (at most two), added in order (kFast: unrolled,
+  // clamped indices, no branch)
+  template <bool kFast>
+  __device__ double grow_dot(int i, int k, const double* xu, double s) const {
+    const int n = T->gr_n[k];
+    if constexpr (kFast) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int tt = t < n ? t : 0;
+        const double p_ = G(i, T->gr_off[k][tt]) * xu[T->gr_col[k][tt]];
+        s += t < n ? p_ : 0.0;
+      }
+    } else {
+      for (int t = 0; t < n; ++t) s += G(i, T->gr_off[k][t]) * xu[T->gr_col[k][t]];
+    }
+    return s;
   }
   // s + sum_t AV[b + t] * v[idx[t]] over the n <= NMAX entries of a CCS column, added in order
   // (kFast: unrolled, clamped indices, no branch)
@@ -271,13 +298,13 @@ struct SolverCtx {
   template <bool kK>
   __device__ void couplings() {
     if (CV)
-      for (int e = lane; e < 36 * (N - 1); e += 64) {
+      for (int e = lane; e < 36 * (N - 1); e += nt) {
         const int i = e / 36 + 1, o = e % 36, j = T->xb_j[o];
         CV[e] = T->xb_r[o] >= 0 ? AV[a_xblock(i) + o] * Pv(i - 1, j) / phix(i, j) : 0.0;
       }
     if constexpr (kK) {
       if (KX)
-        for (int e = lane; e < 78 * N; e += 64) {
+        for (int e = lane; e < 78 * N; e += nt) {
           const int i = e / 78, l = e % 78;
           int r = 0;
           while ((r + 1) * (r + 2) / 2 <= l) ++r;
@@ -286,6 +313,20 @@ struct SolverCtx {
     }
   }
   __device__ double G(int i, int q) const { return GV[28 * i + q]; }
+  // sum / min over the team (wave partials combined in wave order; one wave: wave_sum / wave_min)
+  template <bool kMin>
+  __device__ double team_reduce(double v) const {
+    v = kMin ? wave_min(v) : wave_sum(v);
+    if (nt == 64) return v;
+    __syncthreads();  // the previous reduction's reads of RD are done
+    if ((lane & 63) == 0) RD[lane >> 6] = v;
+    __syncthreads();
+    double r = RD[0];
+    for (int w = 1; w < nt / 64; ++w) r = kMin ? fmin(r, RD[w]) : r + RD[w];
+    return r;
+  }
+  __device__ double team_sum(double v) const { return team_reduce<false>(v); }
+  __device__ double team_min(double v) const { return team_reduce<true>(v); }
   // S_{i,i-1} at x_i's CCS offset o (CV, or formed on the fly where CV did not fit)
   __device__ double cpl(int i, int o) const {
     if (CV) return CV[a_xblock(i) + o];
@@ -306,7 +347,7 @@ struct SolverCtx {
   // rx = Qx + f + G^T z + A^T y ; re = A x - b ; rs = G x + s - h ; returns mu = s'z/m
   template <bool kFast = false>
   __device__ double residuals() {
-    for (int c = lane; c < nz; c += 64) {
+    for (int c = lane; c < nz; c += nt) {
       double v = HV[c] * X[c] + fg[c];
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
@@ -332,7 +373,7 @@ struct SolverCtx {
       }
       RX[c] = v;
     }
-    for (int e = lane; e < p; e += 64) {
+    for (int e = lane; e < p; e += nt) {
       double v = 0.0;
       if (e < 12 * N) {
         const int i = e / 12, r = e % 12;
@@ -346,22 +387,21 @@ struct SolverCtx {
       RE[e] = v - bg[e];
     }
     double sz = 0.0;
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += nt) {
       const int i = q / 16, k = q % 16;
       double v = 0.0;
-      for (int t = 0; t < T->gr_n[k]; ++t)
-        v += G(i, T->gr_off[k][t]) * X[12 * N + 12 * i + T->gr_col[k][t]];
+      v = grow_dot<kFast>(i, k, X + 12 * N + 12 * i, v);
       RS[q] = (v + S[q]) - hg[q];
       sz += S[q] * Z[q];
     }
     __syncthreads();
-    return wave_sum(sz) / m;
+    return team_sum(sz) / m;
   }
 
   // ---------------------------------------------------------------------- factorise ----
   template <bool kFast = false>
   __device__ void factor() {
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += nt) {
       const double si = 1.0 / S[q];
       const double w = si * Z[q] + kDelta;  // S^-1 Z + delta I (sparse_pdipm_solver.py:427)
       SI[q] = si;
@@ -370,7 +410,7 @@ struct SolverCtx {
     }
     __syncthreads();
     // Phi_u foot blocks (lane per (stage, foot)) and decoupled scalars (lane per stage)
-    for (int task = lane; task < 3 * N; task += 64) {
+    for (int task = lane; task < 3 * N; task += nt) {
       if (task < 2 * N) {
       const int i = task >> 1, f = task & 1;
       double a[10];
@@ -409,7 +449,7 @@ struct SolverCtx {
     }
     __syncthreads();
     // diagonal dual blocks S_ii (all stages in parallel), packed lower 78 per stage
-    for (int e = lane; e < 78 * N; e += 64) {
+    for (int e = lane; e < 78 * N; e += nt) {
       const int i = e / 78, l = e % 78;
       int r = 0;
       while ((r + 1) * (r + 2) / 2 <= l) ++r;
@@ -550,11 +590,10 @@ struct SolverCtx {
   // refining the affine direction).
   template <bool kFast = false>
   __device__ void refine_rhs() {
-    for (int q = lane; q < m; q += 64) {  // step 0 (rows 2 and 3)
+    for (int q = lane; q < m; q += nt) {  // step 0 (rows 2 and 3)
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      for (int t = 0; t < T->gr_n[k]; ++t)
-        gd += G(i, T->gr_off[k][t]) * TV[12 * N + 12 * i + T->gr_col[k][t]];
+      gd = grow_dot<kFast>(i, k, TV + 12 * N + 12 * i, gd);
       const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
       const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
       const double qc = DI[q] * (e2 - WD[q] * e3);
@@ -563,9 +602,9 @@ struct SolverCtx {
       DZ[q] = DZ[q] + qc;
     }
     __syncthreads();
-    for (int e = lane; e < nz; e += 64) xsg[e] = TV[e];
-    for (int e = lane; e < p; e += 64) ysg[e] = DY[e];
-    for (int c = lane; c < nz; c += 64) {
+    for (int e = lane; e < nz; e += nt) xsg[e] = TV[e];
+    for (int e = lane; e < p; e += nt) ysg[e] = DY[e];
+    for (int c = lane; c < nz; c += nt) {
       double v = (HV[c] + kBeta) * TV[c] + RX[c];
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
@@ -591,7 +630,7 @@ struct SolverCtx {
       }
       RX[c] = v;
     }
-    for (int e = lane; e < p; e += 64) {
+    for (int e = lane; e < p; e += nt) {
       double v = 0.0;
       if (e < 12 * N) {
         const int i = e / 12, r = e % 12;
@@ -617,10 +656,10 @@ struct SolverCtx {
   template <bool kFast = false>
   __device__ void solve(bool ref = false) {
     if (!ref)
-      for (int q = lane; q < m; q += 64) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
+      for (int q = lane; q < m; q += nt) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
     __syncthreads();
     // r1~ = r1 - G^T VV
-    for (int c = lane; c < nz; c += 64) {
+    for (int c = lane; c < nz; c += nt) {
       double v = -RX[c];
       if (c >= 12 * N && !ref) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
@@ -632,8 +671,8 @@ struct SolverCtx {
     }
     __syncthreads();
     // t = Phi^-1 r1~ (x: diagonal; u: foot blocks, scalars, x-moment pairs)
-    for (int c = lane; c < 12 * N; c += 64) TV[c] = R1T[c] / phix(c / 12 + 1, c % 12);
-    for (int task = lane; task < 3 * N; task += 64) {
+    for (int c = lane; c < 12 * N; c += nt) TV[c] = R1T[c] / phix(c / 12 + 1, c % 12);
+    for (int task = lane; task < 3 * N; task += nt) {
       if (task < 2 * N) {
       const int i = task >> 1, f = task & 1;
       const double* ph = PH + 24 * i + 10 * f;
@@ -660,7 +699,7 @@ struct SolverCtx {
     }
     __syncthreads();
     // g = A_dyn t - r4_dyn
-    for (int e = lane; e < 12 * N; e += 64) {
+    for (int e = lane; e < 12 * N; e += nt) {
       const int i = e / 12, r = e % 12;
       double v = 0.0;
       if (i >= 1) v += mrow(i, r, TV + 12 * (i - 1));
@@ -776,7 +815,7 @@ struct SolverCtx {
     __syncthreads();
     PROF_ADD_CTX((*this), 5);
     // dx = t - Phi^-1 A_dyn^T dy ; x-moment duals from the exact 2x2 elimination
-    for (int c = lane; c < 12 * N; c += 64) {
+    for (int c = lane; c < 12 * N; c += nt) {
       const int k = c / 12 + 1, j = c % 12;
       double aty;
       if (k < N) {
@@ -788,17 +827,19 @@ struct SolverCtx {
       }
       TV[c] = ref ? xsg[c] + (TV[c] - aty / phix(k, j)) : TV[c] - aty / phix(k, j);
     }
-    for (int task = lane; task < 3 * N; task += 64) {
+    // (A_dyn^T dy) of every u column, one column per thread, into WV (dead after the chains): the
+    // per-(stage, foot) tasks below then read them instead of each summing four columns in a row
+    for (int c = lane; c < 12 * N; c += nt) {
+      const int i = c / 12, j = c % 12;
+      WV[c] = col_dot<kFast, 8>(a_ublock(N, i) + T->cpu[j], T->su_n[j], T->su[j], QV + 12 * i, 0.0);
+    }
+    __syncthreads();
+    for (int task = lane; task < 3 * N; task += nt) {
       // u columns: per (stage, foot) block or per stage scalars
       const bool foot = task < 2 * N;
       const int i = foot ? (task >> 1) : task - 2 * N;
       const int b = 12 * N + 12 * i;
-      auto aty_u = [&](int j) {
-        const int ub = a_ublock(N, i) + T->cpu[j];
-        double a = 0.0;
-        a = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], QV + 12 * i, a);
-        return a;
-      };
+      auto aty_u = [&](int j) { return WV[12 * i + j]; };
       if (foot) {
         const int f = task & 1;
         const double* ph = PH + 24 * i + 10 * f;
@@ -828,14 +869,13 @@ struct SolverCtx {
         DY[12 * N + 2 * i + 1] = (e9 * rho9 - p9 * r4b) / (p9 * kDelta + e9 * e9);
       }
     }
-    for (int e = lane; e < 12 * N; e += 64) DY[e] = QV[e];
+    for (int e = lane; e < 12 * N; e += nt) DY[e] = QV[e];
     __syncthreads();
     // dz = D^-1 (r2 - W r3) + Lam G dx ; ds = r3 - G dx + delta dz
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += nt) {
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      for (int t = 0; t < T->gr_n[k]; ++t)
-        gd += G(i, T->gr_off[k][t]) * TV[12 * N + 12 * i + T->gr_col[k][t]];
+      gd = grow_dot<kFast>(i, k, TV + 12 * N + 12 * i, gd);
       const double dz = VV[q] + DI[q] * WD[q] * gd;
       DZ[q] = dz;
       DS[q] = -RS[q] - gd + kDelta * dz;
@@ -850,7 +890,7 @@ struct SolverCtx {
   __device__ void refine() {
     for (int step = 0; step < kRefineSteps; ++step) {
       if (step > 0) {
-        for (int e = lane; e < p; e += 64) DY[e] = ysg[e] + DY[e];
+        for (int e = lane; e < p; e += nt) DY[e] = ysg[e] + DY[e];
         SRBD_GCALL(this->template residuals<kInl>());
       }
       SRBD_GCALL(this->template refine_rhs<kInl>());
@@ -861,13 +901,13 @@ struct SolverCtx {
   // fmax(fmin(1, 0.99 * min_i if_else(dv_i < 0, -v_i/dv_i, 1)), 1e-12)  (:460-467)
   __device__ double step_length(const double* v, const double* dv) const {
     double mn = INFINITY;
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += nt) {
       const bool c = dv[q] < 0.0;
       const double a = -v[q] / dv[q];
       const double cand = (c ? a : 0.0) + (!c ? 1.0 : 0.0);
       mn = fmin(mn, cand);
     }
-    mn = wave_min(mn);
+    mn = team_min(mn);
     return fmax(fmin(1.0, 0.99 * mn), 1e-12);
   }
 };
@@ -894,6 +934,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   C.p = 14 * N;
   C.nd = 12 * N;
   C.lane = lane_in;
+  C.nt = kInl ? kGeneralThreads : 64;
   {
     int used = 0;
     auto place = [&](double*& ptr, int off, int n) {
@@ -914,14 +955,14 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       static_assert(sizeof(Tables) % 2 == 0 && alignof(Tables) <= 16, "Tables copy");
       const uint16_t* src = reinterpret_cast<const uint16_t*>(&c_tab);
       uint16_t* dst = reinterpret_cast<uint16_t*>(tb);
-      for (int w = lane_in; w < (int)(sizeof(Tables) / 2); w += 64) dst[w] = src[w];
+      for (int w = lane_in; w < (int)(sizeof(Tables) / 2); w += C.nt) dst[w] = src[w];
     }
     if (Lo.CV >= 0) place(C.CV, Lo.CV, 36 * N);
     else C.CV = nullptr;
     C.KX = nullptr;
     if constexpr (kInl)
       if (Lo.KX >= 0) place(C.KX, Lo.KX, 78 * N);
-    place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 448); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
+    place(C.DV, Lo.DV, 78 * N); place(C.SC, Lo.SC, 448); place(C.RD, Lo.RD, 8); place(C.QV, Lo.QV, nd); place(C.WV, Lo.WV, nd);
     place(C.PH, Lo.PH, 24 * N); place(C.TV, Lo.TV, nz); place(C.R1T, Lo.R1T, nz);
     place(C.DI, Lo.DI, m); place(C.WD, Lo.WD, m); place(C.SI, Lo.SI, m); place(C.VV, Lo.VV, m);
     place(C.R2, Lo.R2, m); place(C.DS, Lo.DS, m); place(C.DZ, Lo.DZ, m); place(C.DY, Lo.DY, p);
@@ -929,7 +970,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     place(C.RX, Lo.RX, nz); place(C.RS, Lo.RS, m); place(C.RE, Lo.RE, p);
     place(C.HV, Lo.HV, nz); place(C.GV, Lo.GV, 28 * N); place(C.AV, Lo.AV, 122 * N - 24);
   }
-  const int lane = C.lane, nz = C.nz, m = C.m, p = C.p;
+  const int lane = C.lane, nz = C.nz, m = C.m, p = C.p, nt = C.nt;
   const int nA = nnz_A(N), nG = 28 * N;
   const double* Hg = solver_in(args, 0) + (size_t)env * nz;
   const double* Gg = solver_in(args, 1) + (size_t)env * nG;
@@ -939,28 +980,28 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   C.bg = solver_in(args, 5) + (size_t)env * p;
   C.xsg = solver_out(args, 0) + (size_t)env * nz;
   C.ysg = solver_out(args, 3) + (size_t)env * p;
-  for (int e = lane; e < nA; e += 64) C.AV[e] = Ag[e];
-  for (int e = lane; e < nG; e += 64) C.GV[e] = Gg[e];
-  for (int e = lane; e < nz; e += 64) C.HV[e] = Hg[e];
+  for (int e = lane; e < nA; e += nt) C.AV[e] = Ag[e];
+  for (int e = lane; e < nG; e += nt) C.GV[e] = Gg[e];
+  for (int e = lane; e < nz; e += nt) C.HV[e] = Hg[e];
   if (args.init_mode == 2) {  // _ccs cold start (sparse_pdipm_solver.py:30-35)
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
-    for (int e = lane; e < nz; e += 64) C.X[e] = xg[e];
+    for (int e = lane; e < nz; e += nt) C.X[e] = xg[e];
     __syncthreads();
-    for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - ccs_gx(Gg, e, C.X + 12 * N), 1.0); C.Z[e] = 1.0; }
-    for (int e = lane; e < p; e += 64) C.Y[e] = 0.0;
+    for (int e = lane; e < m; e += nt) { C.S[e] = fmax(C.hg[e] - ccs_gx(Gg, e, C.X + 12 * N), 1.0); C.Z[e] = 1.0; }
+    for (int e = lane; e < p; e += nt) C.Y[e] = 0.0;
   } else if (args.init_mode == 0) {
     const double* xg = solver_in(args, 6) + (size_t)env * nz;
     const double* sg = solver_in(args, 7) + (size_t)env * m;
     const double* zg = solver_in(args, 8) + (size_t)env * m;
     const double* yg = solver_in(args, 9) + (size_t)env * p;
-    for (int e = lane; e < nz; e += 64) C.X[e] = xg[e];
-    for (int e = lane; e < m; e += 64) { C.S[e] = sg[e]; C.Z[e] = zg[e]; }
-    for (int e = lane; e < p; e += 64) C.Y[e] = yg[e];
+    for (int e = lane; e < nz; e += nt) C.X[e] = xg[e];
+    for (int e = lane; e < m; e += nt) { C.S[e] = sg[e]; C.Z[e] = zg[e]; }
+    for (int e = lane; e < p; e += nt) C.Y[e] = yg[e];
   } else {
     // mpc_controller_cusadi.py:138-141: x = 0, s = max(d - G 0, 1), z = 1, y = y0
-    for (int e = lane; e < nz; e += 64) C.X[e] = 0.0;
-    for (int e = lane; e < m; e += 64) { C.S[e] = fmax(C.hg[e] - 0.0, 1.0); C.Z[e] = 1.0; }
-    for (int e = lane; e < p; e += 64) C.Y[e] = args.y0;
+    for (int e = lane; e < nz; e += nt) C.X[e] = 0.0;
+    for (int e = lane; e < m; e += nt) { C.S[e] = fmax(C.hg[e] - 0.0, 1.0); C.Z[e] = 1.0; }
+    for (int e = lane; e < p; e += nt) C.Y[e] = args.y0;
   }
   __syncthreads();
   C.template couplings<kInl>();
@@ -975,16 +1016,16 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     PROF_ADD_CTX(C, 0);
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
       double a = 0.0, b = 0.0, c = 0.0;
-      for (int e = lane; e < nz; e += 64) a += C.RX[e] * C.RX[e];
-      for (int e = lane; e < m; e += 64) b += C.RS[e] * C.RS[e];
-      for (int e = lane; e < p; e += 64) c += C.RE[e] * C.RE[e];
-      res0 = sqrt(wave_sum(a));
-      res1 = sqrt(wave_sum(b));
-      res2 = sqrt(wave_sum(c));
+      for (int e = lane; e < nz; e += nt) a += C.RX[e] * C.RX[e];
+      for (int e = lane; e < m; e += nt) b += C.RS[e] * C.RS[e];
+      for (int e = lane; e < p; e += nt) c += C.RE[e] * C.RE[e];
+      res0 = sqrt(C.team_sum(a));
+      res1 = sqrt(C.team_sum(b));
+      res2 = sqrt(C.team_sum(c));
     }
     SRBD_GCALL(C.template factor<kInl>());
     // affine: r2 = -(S^-1 (s o z))
-    for (int q = lane; q < m; q += 64) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
+    for (int q = lane; q < m; q += nt) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
     SRBD_GCALL(C.template solve<kInl>());
     SRBD_GCALL(C.template refine<kInl>());  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
@@ -994,12 +1035,12 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     SRBD_GCALL(ap = C.step_length(C.S, C.DS));
     SRBD_GCALL(ad = C.step_length(C.Z, C.DZ));
     double sza = 0.0;
-    for (int q = lane; q < m; q += 64) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
-    const double mu_aff = wave_sum(sza) / m;
+    for (int q = lane; q < m; q += nt) sza += (C.S[q] + ap * C.DS[q]) * (C.Z[q] + ad * C.DZ[q]);
+    const double mu_aff = C.team_sum(sza) / m;
     const double sigma = pow(mu_aff / mu, 3.0);
     // combined rhs: r2 = -(S^-1 (s o z)) - S^-1 (s o z + ds_a o dz_a - sigma mu e)
     __syncthreads();
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += nt) {
       const double rc = C.S[q] * C.Z[q] + C.DS[q] * C.DZ[q] - sigma * mu * 1.0;
       C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q])) + -(C.SI[q] * rc);
     }
@@ -1012,16 +1053,16 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
     floor_hit = apc <= 1e-12 || adc <= 1e-12;  // the last iteration's value is reported
     __syncthreads();
     double szn = 0.0;
-    for (int e = lane; e < nz; e += 64) C.X[e] = C.X[e] + apc * C.TV[e];
-    for (int q = lane; q < m; q += 64) {
+    for (int e = lane; e < nz; e += nt) C.X[e] = C.X[e] + apc * C.TV[e];
+    for (int q = lane; q < m; q += nt) {
       const double sn = fmax(C.S[q] + apc * C.DS[q], 1e-8);
       const double zn = fmax(fmax(C.Z[q] + adc * C.DZ[q], 1e-8), 1e-8);
       C.S[q] = sn;
       C.Z[q] = zn;
       szn += sn * zn;
     }
-    for (int e = lane; e < p; e += 64) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
-    mu_new = wave_sum(szn) / m;
+    for (int e = lane; e < p; e += nt) C.Y[e] = C.Y[e] + adc * (C.ysg[e] + C.DY[e]);  // saved + correction
+    mu_new = C.team_sum(szn) / m;
     __syncthreads();
     PROF_ADD_CTX(C, 8);
   }
@@ -1032,9 +1073,9 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   double* yo = solver_out(args, 3) + (size_t)env * p;
   double* ro = solver_out(args, 4) + (size_t)env * 4;
   double* mo = solver_out(args, 5) + (size_t)env;
-  for (int e = lane; e < nz; e += 64) xo[e] = C.X[e];
-  for (int e = lane; e < m; e += 64) { so[e] = C.S[e]; zo[e] = C.Z[e]; }
-  for (int e = lane; e < p; e += 64) yo[e] = C.Y[e];
+  for (int e = lane; e < nz; e += nt) xo[e] = C.X[e];
+  for (int e = lane; e < m; e += nt) { so[e] = C.S[e]; zo[e] = C.Z[e]; }
+  for (int e = lane; e < p; e += nt) yo[e] = C.Y[e];
   if (lane == 0) {
     ro[0] = res0;
     ro[1] = res1;
@@ -1044,10 +1085,10 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   }
   if (args.status) {
     bool nf = lane == 0 && not_finite(mu_new);
-    for (int e = lane; e < nz; e += 64) nf = nf || not_finite(C.X[e]);
-    for (int e = lane; e < m; e += 64) nf = nf || not_finite(C.S[e]) || not_finite(C.Z[e]);
-    for (int e = lane; e < p; e += 64) nf = nf || not_finite(C.Y[e]);
-    nf = __any(nf);
+    for (int e = lane; e < nz; e += nt) nf = nf || not_finite(C.X[e]);
+    for (int e = lane; e < m; e += nt) nf = nf || not_finite(C.S[e]) || not_finite(C.Z[e]);
+    for (int e = lane; e < p; e += nt) nf = nf || not_finite(C.Y[e]);
+    nf = C.team_sum(nf ? 1.0 : 0.0) > 0.0;
     if (lane == 0)
       args.status[env] = status_bits | (nf ? kStatusNonFinite : 0) | (floor_hit ? kStatusStepFloor : 0);
   }
@@ -1101,7 +1142,7 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
 
 #ifndef SRBD_NO_GENERAL_KERNEL  // srbd_reg20.hip (second unit) does not define it again
 // One workgroup per QP (the "general" solver path, srbd_set_solver_path(1))
-__global__ __launch_bounds__(64) void pdipm_kernel(SolverArgs args) {
+__global__ __launch_bounds__(kGeneralThreads) void pdipm_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   if ((int)blockIdx.x < args.batch) pdipm_general_at<true>(args, blockIdx.x, smem, threadIdx.x);
 }

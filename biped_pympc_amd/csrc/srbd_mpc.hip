@@ -216,7 +216,7 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   const size_t lds = solver_lds_bytes(a.N);
   if (lds > 160 * 1024) return set_error(kErrInvalid, "horizon too large for the LDS-resident solver");
   if (int rc = ensure_lds_attr((const void*)srbd::pdipm_kernel, lds, cfg_general)) return rc;
-  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(64), lds, s, a);
+  hipLaunchKernelGGL(srbd::pdipm_kernel, dim3(a.batch), dim3(srbd::kGeneralThreads), lds, s, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error((int)e, "pdipm_kernel launch");
 }
