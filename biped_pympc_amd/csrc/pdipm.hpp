@@ -84,6 +84,28 @@ constexpr Tables kTabs = make_tables();
 // chains of SolverCtx (as those of pdipm_srbd.hpp FastCtx) rely on: row c holds {c}, plus {6, 7, 8}
 // for c < 3 and {c + 6} for 3 <= c < 6; and pi C^T pi^T (pi = perm12) has the same pattern, so the
 // backward group runs the forward group's instructions.
+// G's CCS columns are contiguous runs of at most 8 entries (gcol_dot's unrolled form)
+constexpr bool g_columns_ok() {
+  for (int q = 0; q < 28; ++q)
+    if (q < kTabs.gcp[kTabs.gcol[q]] || q >= kTabs.gcp[kTabs.gcol[q]] + kTabs.gcn[kTabs.gcol[q]]) return false;
+  for (int j = 0; j < 12; ++j)
+    if (kTabs.gcn[j] > 8) return false;
+  return true;
+}
+static_assert(g_columns_ok(), "G column runs");
+// the foot rows of G: row 8 + k (right foot) has row k's (left foot) pattern, mirrored foot columns
+constexpr bool g_feet_ok() {
+  for (int k = 0; k < 8; ++k) {
+    if (kTabs.gr_n[k] != kTabs.gr_n[8 + k]) return false;
+    for (int t = 0; t < kTabs.gr_n[k]; ++t) {
+      const int a = kTabs.gr_col[k][t], b = kTabs.gr_col[8 + k][t];
+      if (kTabs.col_foot[a] != 0 || kTabs.col_foot[b] != 1 || kTabs.col_pos[a] != kTabs.col_pos[b]) return false;
+    }
+  }
+  return true;
+}
+static_assert(g_feet_ok(), "G foot rows");
+
 constexpr bool coupling_pattern_ok() {
   for (int r = 0; r < 12; ++r)
     for (int j = 0; j < 12; ++j) {
@@ -203,22 +225,22 @@ struct SolverCtx {
   }
   __device__ double E6(int i) const { return AV[a_ublock(N, i) + kTabs.e6]; }
   __device__ double E9(int i) const { return AV[a_ublock(N, i) + kTabs.e9]; }
-  // f(q, k) for the G entries of u column j (CCS value q, stage-local row k) in CCS order: the 28
-  // candidate entries unrolled against the compile-time tables (no table loads; the same summation
-  // order as the loop over the column's entries)
-  // acc += sum over the G entries of u column j of stage i (CCS order) of value * v[stage-local row].
-  // kFast (the general kernel, everything inlined): the 28 candidates unrolled against the
-  // compile-time tables; otherwise (the fallback's out-of-line phases, whose register use the calling
-  // stage-invariant kernel has to save around the call) the plain loop over the tables.
+  // acc += sum over the G entries of u column j of stage i (CCS order: the column's contiguous run
+  // gcp[j] .. + gcn[j]) of value * v[stage-local row]. kFast (the general kernel, everything inlined):
+  // the at most 8 entries unrolled with clamped indices, no branch; otherwise (the fallback's
+  // out-of-line phases) the plain loop.
   template <bool kFast>
   __device__ void gcol_dot(int i, int j, const double* v, double& acc) const {
+    const int b = T->gcp[j], n = T->gcn[j];
     if constexpr (kFast) {
 #pragma unroll
-      for (int q = 0; q < 28; ++q)
-        if (kTabs.gcol[q] == j) acc += G(i, q) * v[kTabs.grow[q]];
+      for (int t = 0; t < 8; ++t) {
+        const int q = b + (t < n ? t : 0);
+        const double p_ = G(i, q) * v[T->grow[q]];
+        acc += t < n ? p_ : 0.0;
+      }
     } else {
-      for (int q = 0; q < 28; ++q)
-        if (T->gcol[q] == j) acc += G(i, q) * v[T->grow[q]];
+      for (int t = 0; t < n; ++t) acc += G(i, b + t) * v[T->grow[b + t]];
     }
   }
   // s + (G_i xu)_k over inequality row k's entries (at most two), added in order (kFast: unrolled,
@@ -418,6 +440,26 @@ struct SolverCtx {
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? phiu(i, T->foot_col[f][r]) : 0.0;
+      if constexpr (kFast) {  // compile-time row patterns (the same for both feet): no table lookups
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = 16 * i + 8 * f + k;
+          const double lam = DI[q] * WD[q];
+          double g4[4] = {0.0, 0.0, 0.0, 0.0};
+          int nzm = 0;
+#pragma unroll
+          for (int t = 0; t < kTabs.gr_n[k]; ++t) {
+            const int pos = kTabs.col_pos[kTabs.gr_col[k][t]];
+            g4[pos] = G(i, f ? kTabs.gr_off[8 + k][t] : kTabs.gr_off[k][t]);
+            nzm |= 1 << pos;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c <= r; ++c)
+              if ((nzm >> r) & (nzm >> c) & 1) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
+        }
+      } else
       for (int k = 0; k < 8; ++k) {
         const int q = 16 * i + 8 * f + k;
         const double lam = DI[q] * WD[q];

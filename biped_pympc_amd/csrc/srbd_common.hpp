@@ -58,6 +58,8 @@ struct Tables {
   // column -> (foot, position) or -1 for the four decoupled columns {6,8,9,11}
   int8_t col_foot[12];
   int8_t col_pos[12];
+  // G by column: u column j's entries are gcp[j] .. gcp[j] + gcn[j] - 1 in CCS order (at most 8)
+  int8_t gcp[12], gcn[12];
 };
 
 // kSiiOrder: scripts/sii_order.py (a seeded search over the order within each class: the extra
@@ -150,6 +152,16 @@ constexpr Tables make_tables() {
       ++g;
     }
   }
+  for (int j = 0; j < 12; ++j) {
+    t.gcn[j] = 0;
+    t.gcp[j] = -1;
+  }
+  for (int q = 0; q < 28; ++q) {
+    if (t.gcp[t.gcol[q]] < 0) t.gcp[t.gcol[q]] = (int8_t)q;
+    t.gcn[t.gcol[q]]++;
+  }
+  for (int j = 0; j < 12; ++j)
+    if (t.gcp[j] < 0) t.gcp[j] = 0;
   for (int k = 0; k < 16; ++k) t.gr_n[k] = 0;
   for (int q = 0; q < 28; ++q) {
     const int k = t.grow[q];
