@@ -226,53 +226,36 @@ struct SolverCtx {
   __device__ double E6(int i) const { return AV[a_ublock(N, i) + kTabs.e6]; }
   __device__ double E9(int i) const { return AV[a_ublock(N, i) + kTabs.e9]; }
   // acc += sum over the G entries of u column j of stage i (CCS order: the column's contiguous run
-  // gcp[j] .. + gcn[j]) of value * v[stage-local row]. kFast (the general kernel, everything inlined):
-  // the at most 8 entries unrolled with clamped indices, no branch; otherwise (the fallback's
-  // out-of-line phases) the plain loop.
-  template <bool kFast>
+  // gcp[j] .. + gcn[j]) of value * v[stage-local row]: the at most 8 entries unrolled with clamped
+  // indices, no branch (the sparse sums below likewise add their entries in order)
   __device__ void gcol_dot(int i, int j, const double* v, double& acc) const {
     const int b = T->gcp[j], n = T->gcn[j];
-    if constexpr (kFast) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int q = b + (t < n ? t : 0);
-        const double p_ = G(i, q) * v[T->grow[q]];
-        acc += t < n ? p_ : 0.0;
-      }
-    } else {
-      for (int t = 0; t < n; ++t) acc += G(i, b + t) * v[T->grow[b + t]];
+    for (int t = 0; t < 8; ++t) {
+      const int q = b + (t < n ? t : 0);
+      const double p_ = G(i, q) * v[T->grow[q]];
+      acc += t < n ? p_ : 0.0;
     }
   }
-  // s + (G_i xu)_k over inequality row k's entries (at most two), added in order (kFast: unrolled,
-  // clamped indices, no branch)
-  template <bool kFast>
+  // s + (G_i xu)_k over inequality row k's entries (at most two)
   __device__ double grow_dot(int i, int k, const double* xu, double s) const {
     const int n = T->gr_n[k];
-    if constexpr (kFast) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int tt = t < n ? t : 0;
-        const double p_ = G(i, T->gr_off[k][tt]) * xu[T->gr_col[k][tt]];
-        s += t < n ? p_ : 0.0;
-      }
-    } else {
-      for (int t = 0; t < n; ++t) s += G(i, T->gr_off[k][t]) * xu[T->gr_col[k][t]];
+    for (int t = 0; t < 2; ++t) {
+      const int tt = t < n ? t : 0;
+      const double p_ = G(i, T->gr_off[k][tt]) * xu[T->gr_col[k][tt]];
+      s += t < n ? p_ : 0.0;
     }
     return s;
   }
-  // s + sum_t AV[b + t] * v[idx[t]] over the n <= NMAX entries of a CCS column, added in order
-  // (kFast: unrolled, clamped indices, no branch)
-  template <bool kFast, int NMAX>
+  // s + sum_t AV[b + t] * v[idx[t]] over the n <= NMAX entries of a CCS column
+  template <int NMAX>
   __device__ double col_dot(int b, int n, const int8_t* idx, const double* v, double s) const {
-    if constexpr (kFast) {
 #pragma unroll
-      for (int t = 0; t < NMAX; ++t) {
-        const int tt = t < n ? t : 0;
-        const double p_ = AV[b + tt] * v[idx[tt]];
-        s += t < n ? p_ : 0.0;
-      }
-    } else {
-      for (int t = 0; t < n; ++t) s += AV[b + t] * v[idx[t]];
+    for (int t = 0; t < NMAX; ++t) {
+      const int tt = t < n ? t : 0;
+      const double p_ = AV[b + tt] * v[idx[tt]];
+      s += t < n ? p_ : 0.0;
     }
     return s;
   }
@@ -367,17 +350,16 @@ struct SolverCtx {
 
   // ---------------------------------------------------------------------- residuals ----
   // rx = Qx + f + G^T z + A^T y ; re = A x - b ; rs = G x + s - h ; returns mu = s'z/m
-  template <bool kFast = false>
   __device__ double residuals() {
     for (int c = lane; c < nz; c += nt) {
       double v = HV[c] * X[c] + fg[c];
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
-        gcol_dot<kFast>(i, j, Z + 16 * i, gz);
+        gcol_dot(i, j, Z + 16 * i, gz);
         double ay = 0.0;
         const int ub = a_ublock(N, i) + T->cpu[j];
-        ay = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], Y + 12 * i, ay);
+        ay = col_dot<8>(ub, T->su_n[j], T->su[j], Y + 12 * i, ay);
         if (j == 6) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i];
         if (j == 9) ay += AV[ub + T->su_n[j]] * Y[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
@@ -387,7 +369,7 @@ struct SolverCtx {
         if (k < N) {
           const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * Y[12 * (k - 1) + j];
-          ay = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], Y + 12 * k, ay);
+          ay = col_dot<4>(xb + 1, T->sx_n[j], T->sx[j], Y + 12 * k, ay);
         } else {
           ay = AV[36 * (N - 1) + j] * Y[12 * (k - 1) + j];
         }
@@ -412,7 +394,7 @@ struct SolverCtx {
     for (int q = lane; q < m; q += nt) {
       const int i = q / 16, k = q % 16;
       double v = 0.0;
-      v = grow_dot<kFast>(i, k, X + 12 * N + 12 * i, v);
+      v = grow_dot(i, k, X + 12 * N + 12 * i, v);
       RS[q] = (v + S[q]) - hg[q];
       sz += S[q] * Z[q];
     }
@@ -421,7 +403,6 @@ struct SolverCtx {
   }
 
   // ---------------------------------------------------------------------- factorise ----
-  template <bool kFast = false>
   __device__ void factor() {
     for (int q = lane; q < m; q += nt) {
       const double si = 1.0 / S[q];
@@ -440,42 +421,25 @@ struct SolverCtx {
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? phiu(i, T->foot_col[f][r]) : 0.0;
-      if constexpr (kFast) {  // compile-time row patterns (the same for both feet): no table lookups
+      // compile-time row patterns (the same for both feet, g_feet_ok): no table lookups, and the
+      // structural zeros of each rank-1 update skipped
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int q = 16 * i + 8 * f + k;
-          const double lam = DI[q] * WD[q];
-          double g4[4] = {0.0, 0.0, 0.0, 0.0};
-          int nzm = 0;
-#pragma unroll
-          for (int t = 0; t < kTabs.gr_n[k]; ++t) {
-            const int pos = kTabs.col_pos[kTabs.gr_col[k][t]];
-            g4[pos] = G(i, f ? kTabs.gr_off[8 + k][t] : kTabs.gr_off[k][t]);
-            nzm |= 1 << pos;
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c <= r; ++c)
-              if ((nzm >> r) & (nzm >> c) & 1) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
-        }
-      } else
       for (int k = 0; k < 8; ++k) {
         const int q = 16 * i + 8 * f + k;
         const double lam = DI[q] * WD[q];
         double g4[4] = {0.0, 0.0, 0.0, 0.0};
-        const int row = 8 * f + k, nrow = T->gr_n[row];
+        int nzm = 0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {  // (at most two entries per row; constant indices into g4: no scratch)
-          const int pos = t < nrow ? T->col_pos[T->gr_col[row][t]] : -1;
-          const double v = t < nrow ? G(i, T->gr_off[row][t]) : 0.0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) g4[b] = pos == b ? v : g4[b];
+        for (int t = 0; t < kTabs.gr_n[k]; ++t) {
+          const int pos = kTabs.col_pos[kTabs.gr_col[k][t]];
+          g4[pos] = G(i, f ? kTabs.gr_off[8 + k][t] : kTabs.gr_off[k][t]);
+          nzm |= 1 << pos;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
+          for (int c = 0; c <= r; ++c)
+            if ((nzm >> r) & (nzm >> c) & 1) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
       }
       sweep_inverse<4>(a);
 #pragma unroll
@@ -496,9 +460,7 @@ struct SolverCtx {
       int r = 0;
       while ((r + 1) * (r + 2) / 2 <= l) ++r;
       const int c = l - r * (r + 1) / 2;
-      double v;
-      if constexpr (kFast) v = KX ? KX[e] : sii_x(i, r, c);
-      else v = sii_x(i, r, c);
+      double v = KX ? KX[e] : sii_x(i, r, c);
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         double vr[4], vc[4];
@@ -630,12 +592,11 @@ struct SolverCtx {
   // RX <- -(e1 - G^T q) (G^T over the updated DZ), RE <- -e4; dx and dy saved to the output rows for
   // solve(true). RX, RE, RS are overwritten (the caller restores them with residuals() after
   // refining the affine direction).
-  template <bool kFast = false>
   __device__ void refine_rhs() {
     for (int q = lane; q < m; q += nt) {  // step 0 (rows 2 and 3)
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      gd = grow_dot<kFast>(i, k, TV + 12 * N + 12 * i, gd);
+      gd = grow_dot(i, k, TV + 12 * N + 12 * i, gd);
       const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
       const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
       const double qc = DI[q] * (e2 - WD[q] * e3);
@@ -651,10 +612,10 @@ struct SolverCtx {
       if (c >= 12 * N) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double gz = 0.0;
-        gcol_dot<kFast>(i, j, DZ + 16 * i, gz);
+        gcol_dot(i, j, DZ + 16 * i, gz);
         double ay = 0.0;
         const int ub = a_ublock(N, i) + T->cpu[j];
-        ay = col_dot<kFast, 8>(ub, T->su_n[j], T->su[j], DY + 12 * i, ay);
+        ay = col_dot<8>(ub, T->su_n[j], T->su[j], DY + 12 * i, ay);
         if (j == 6) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i];
         if (j == 9) ay += AV[ub + T->su_n[j]] * DY[12 * N + 2 * i + 1];
         v = (v + gz) + ay;
@@ -664,7 +625,7 @@ struct SolverCtx {
         if (k < N) {
           const int xb = a_xblock(k) + T->cpx[j];
           ay = AV[xb] * DY[12 * (k - 1) + j];
-          ay = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], DY + 12 * k, ay);
+          ay = col_dot<4>(xb + 1, T->sx_n[j], T->sx[j], DY + 12 * k, ay);
         } else {
           ay = AV[36 * (N - 1) + j] * DY[12 * (k - 1) + j];
         }
@@ -695,7 +656,6 @@ struct SolverCtx {
   // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV, RS from refine_rhs's
   // step 0 carry rows 2 and 3), then dx = saved + correction before dz, ds are formed; DY is the
   // correction.
-  template <bool kFast = false>
   __device__ void solve(bool ref = false) {
     if (!ref)
       for (int q = lane; q < m; q += nt) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
@@ -706,7 +666,7 @@ struct SolverCtx {
       if (c >= 12 * N && !ref) {
         const int i = (c - 12 * N) / 12, j = (c - 12 * N) % 12;
         double g = 0.0;
-        gcol_dot<kFast>(i, j, VV + 16 * i, g);
+        gcol_dot(i, j, VV + 16 * i, g);
         v -= g;
       }
       R1T[c] = v;
@@ -863,7 +823,7 @@ struct SolverCtx {
       if (k < N) {
         const int xb = a_xblock(k) + T->cpx[j];
         aty = AV[xb] * QV[12 * (k - 1) + j];
-        aty = col_dot<kFast, 4>(xb + 1, T->sx_n[j], T->sx[j], QV + 12 * k, aty);
+        aty = col_dot<4>(xb + 1, T->sx_n[j], T->sx[j], QV + 12 * k, aty);
       } else {
         aty = AV[36 * (N - 1) + j] * QV[12 * (k - 1) + j];
       }
@@ -873,7 +833,7 @@ struct SolverCtx {
     // per-(stage, foot) tasks below then read them instead of each summing four columns in a row
     for (int c = lane; c < 12 * N; c += nt) {
       const int i = c / 12, j = c % 12;
-      WV[c] = col_dot<kFast, 8>(a_ublock(N, i) + T->cpu[j], T->su_n[j], T->su[j], QV + 12 * i, 0.0);
+      WV[c] = col_dot<8>(a_ublock(N, i) + T->cpu[j], T->su_n[j], T->su[j], QV + 12 * i, 0.0);
     }
     __syncthreads();
     for (int task = lane; task < 3 * N; task += nt) {
@@ -917,7 +877,7 @@ struct SolverCtx {
     for (int q = lane; q < m; q += nt) {
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      gd = grow_dot<kFast>(i, k, TV + 12 * N + 12 * i, gd);
+      gd = grow_dot(i, k, TV + 12 * N + 12 * i, gd);
       const double dz = VV[q] + DI[q] * WD[q] * gd;
       DZ[q] = dz;
       DS[q] = -RS[q] - gd + kDelta * dz;
@@ -933,10 +893,10 @@ struct SolverCtx {
     for (int step = 0; step < kRefineSteps; ++step) {
       if (step > 0) {
         for (int e = lane; e < p; e += nt) DY[e] = ysg[e] + DY[e];
-        SRBD_GCALL(this->template residuals<kInl>());
+        SRBD_GCALL(this->residuals());
       }
-      SRBD_GCALL(this->template refine_rhs<kInl>());
-      SRBD_GCALL(this->template solve<kInl>(true));
+      SRBD_GCALL(this->refine_rhs());
+      SRBD_GCALL(this->solve(true));
     }
   }
 
@@ -1054,7 +1014,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   PROF_MARK_CTX(C);
   for (int it = 0; it < args.n_iter; ++it) {
     double mu;
-    SRBD_GCALL(mu = C.template residuals<kInl>());
+    SRBD_GCALL(mu = C.residuals());
     PROF_ADD_CTX(C, 0);
     if (it == args.n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses RX, RE)
       double a = 0.0, b = 0.0, c = 0.0;
@@ -1065,13 +1025,13 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       res1 = sqrt(C.team_sum(b));
       res2 = sqrt(C.team_sum(c));
     }
-    SRBD_GCALL(C.template factor<kInl>());
+    SRBD_GCALL(C.factor());
     // affine: r2 = -(S^-1 (s o z))
     for (int q = lane; q < m; q += nt) C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q]));
     __syncthreads();
-    SRBD_GCALL(C.template solve<kInl>());
+    SRBD_GCALL(C.solve());
     SRBD_GCALL(C.template refine<kInl>());  // the affine direction too (pdipm_srbd.hpp main loop: its ds, dz feed sigma)
-    SRBD_GCALL(C.template residuals<kInl>());  // restores RX, RS, RE for the combined solve
+    SRBD_GCALL(C.residuals());  // restores RX, RS, RE for the combined solve
     PROF_ADD_CTX(C, 0);
     double ap, ad;
     SRBD_GCALL(ap = C.step_length(C.S, C.DS));
@@ -1087,7 +1047,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
       C.R2[q] = -(C.SI[q] * (C.S[q] * C.Z[q])) + -(C.SI[q] * rc);
     }
     __syncthreads();
-    SRBD_GCALL(C.template solve<kInl>());
+    SRBD_GCALL(C.solve());
     SRBD_GCALL(C.template refine<kInl>());
     double apc, adc;
     SRBD_GCALL(apc = C.step_length(C.S, C.DS));
