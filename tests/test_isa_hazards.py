@@ -56,7 +56,9 @@ def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
     VGPRs). The fused kernel has no spill at all; the CCS kernel's only ones are the
     whole-wave save of its SGPR-spill register around the call of the in-launch general fallback
     (pdipm.hpp pdipm_general_scratch), which runs for QPs that are not stage-invariant only: no spill
-    or reload instruction elsewhere, and at most 2 such registers."""
+    or reload instruction elsewhere, and at most 2 such registers. And every register kernel stays
+    within 256 VGPRs, its callees included (the kernel's count is the maximum over the call graph: a
+    fallback phase compiled past 256 would take the fast path from 2 waves per SIMD to 1)."""
     from dpp_hazard_check import check
     from kernel_resources import body_spills, resources
     for s in _isa(tmp_path, unit):
@@ -64,6 +66,8 @@ def test_no_dpp_read_within_two_states_of_a_write(tmp_path, unit):
         for name, r in resources(s, "reg_kernel").items():
             n = _reg_horizon(name)
             limit = 24 if "mpc_step" in name else 20
+            if n is not None:
+                assert r["vgpr_count"] <= 256, (name, r)
             if n is not None and n <= limit:
                 if "mpc_step" in name:
                     assert r["vgpr_spill_count"] == 0, (name, r)
