@@ -198,8 +198,8 @@ __device__ inline double ccs_gx(const double* Gv, int q, const double* xu) {
 
 struct SolverCtx {
   int N, nz, m, p, nd, lane;
-  // nt: the threads a QP's row-parallel loops stride over (kGeneralThreads in the general kernel; 64
-  // in the fallback, whose other waves are idle lanes); RD: one reduction partial per wave (LDS)
+  // nt: the threads a QP's row-parallel loops stride over (kGeneralThreads in the general kernel; in
+  // the fallback the calling kernel's threads per QP: 64, 128 or 192); RD: one partial per wave
   int nt;
   double* RD;
   double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,
@@ -916,8 +916,8 @@ struct SolverCtx {
 
 // The general solve of QP `env` with its working set at `smem` (the workgroup's LDS in pdipm_kernel,
 // a slot of the library's global scratch pool when a stage-invariant kernel meets a QP it cannot
-// take). `lane` >= 64 marks an idle lane (the second wave of a two-wave QP): it takes part in every
-// barrier and stores nothing.
+// take). `lane_in` is the thread's index in the QP's team of `nt_in` threads: every wave of the
+// workgroup (two in the general kernel; in the fallback the calling kernel's waves of that QP).
 // `smem`: the QP's working set (the workgroup's LDS in pdipm_kernel, a scratch-pool slot in global
 // memory for the fallback). `lds`, `lds_cap`: LDS the caller can spare (the fallback: the stage-invariant
 // kernel's own LDS, unused by a QP it hands over); the arrays the sequential chains touch go there first
@@ -926,7 +926,8 @@ struct SolverCtx {
 // fallback ~2x slower than the same solve in LDS.)
 template <bool kInl>
 __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env, double* smem, int lane_in,
-                                                 int status_bits = 0, double* lds = nullptr, int lds_cap = 0) {
+                                                 int nt_in, int status_bits = 0, double* lds = nullptr,
+                                                 int lds_cap = 0) {
   const int N = args.N;
   const SolverLayout Lo(N);
   SolverCtx C;
@@ -936,7 +937,7 @@ __device__ __forceinline__ void pdipm_general_at(const SolverArgs& args, int env
   C.p = 14 * N;
   C.nd = 12 * N;
   C.lane = lane_in;
-  C.nt = kInl ? kGeneralThreads : 64;
+  C.nt = nt_in;
   {
     int used = 0;
     auto place = [&](double*& ptr, int off, int n) {
@@ -1112,8 +1113,8 @@ __device__ __forceinline__ const SolverArgs& kernel_args() {
   return *(const SolverArgs*)__builtin_amdgcn_kernarg_segment_ptr();  // constant -> generic address space
 }
 // `lds` / `lds_doubles`: the calling workgroup's LDS (all of it: the QP handed over never started the
-// fast path); its first int is where a multi-wave QP's waves agree on the slot (wave 0 takes it; the
-// other waves run the solve as idle lanes but read the slot's memory, so they must see the same one),
+// fast path); its first int is where a multi-wave QP's waves agree on the slot (wave 0 takes it; all
+// of the QP's waves then run the solve as one team over the slot's memory),
 // the rest holds the chain arrays of the general solve (pdipm_general_at). The pool has as many slots
 // as the device holds resident workgroups of any stage-invariant kernel, so a slot is free at the first
 // or an early probe and no workgroup waits on another's solve.
@@ -1134,9 +1135,8 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
   slot = *xchg;
   __syncthreads();  // every wave has the slot before the general solve reuses the LDS
   __threadfence();
-  const int lane = threadIdx.x < 64 ? (int)threadIdx.x : (1 << 20);
-  pdipm_general_at<false>(args, env, args.scratch + (size_t)slot * args.scratch_stride, lane,
-                          kStatusFallback, lds, lds_doubles);
+  pdipm_general_at<false>(args, env, args.scratch + (size_t)slot * args.scratch_stride, threadIdx.x,
+                          blockDim.x, kStatusFallback, lds, lds_doubles);
   __syncthreads();
   __threadfence();
   if (threadIdx.x == 0) atomicExch(&args.scratch_locks[(size_t)slot * kLockStride], 0);
@@ -1146,7 +1146,7 @@ __device__ __attribute__((noinline)) void pdipm_general_scratch(const SolverArgs
 // One workgroup per QP (the "general" solver path, srbd_set_solver_path(1))
 __global__ __launch_bounds__(kGeneralThreads) void pdipm_kernel(SolverArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  if ((int)blockIdx.x < args.batch) pdipm_general_at<true>(args, blockIdx.x, smem, threadIdx.x);
+  if ((int)blockIdx.x < args.batch) pdipm_general_at<true>(args, blockIdx.x, smem, threadIdx.x, kGeneralThreads);
 }
 #endif  // SRBD_NO_GENERAL_KERNEL
 
