@@ -50,8 +50,9 @@ NODE_GPUS = int(os.environ.get("SRBD_NODE_GPUS", "8"))  # GPUs sharing one host 
 
 def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1,
-                   help="ranks (one per GPU); > 1 without WORLD_SIZE set: bench.py starts them itself")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU; default: WORLD_SIZE under an external launcher, else 1); > 1 "
+                        "without WORLD_SIZE set: bench.py starts them itself")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch-per-gpu", type=int, default=4096)
@@ -67,6 +68,8 @@ def parse(argv=None):
     p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
     p.add_argument("--no-dropin", action="store_true",
                    help="skip the reference caller's CusADi schedule leg (1 former + 4 x 5-iteration evaluate)")
+    p.add_argument("--no-config3", action="store_true",
+                   help="skip the BASELINE config-3 leg (fused N = 20, B = 4096, K = 10 kernel + oracle sample)")
     p.add_argument("--dump-u0", default=None,
                    help="rank 0 saves the gathered u0 (global env order) of the last timed step as .npy")
     return p.parse_args(argv)
@@ -264,12 +267,32 @@ def run_timed(sh, inputs, a, dist, world, dev):
     sync()
     if dist is not None:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = own = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, last[0]
+    return elapsed, last[0], own
+
+
+def rank_spread(dist, dev, solve_ms: float, gather_ms: float, elapsed_s: float):
+    """Per-rank figures of an N > 1 run, gathered to every rank: each rank's shard solve (its own
+    step kernel, timed alone), its u0 gather (timed alone) and its own clock over the timed steps, so
+    a sub-linear point can be attributed to a slow rank or to the gather. None without a group."""
+    if dist is None:
+        return None
+    world = dist.get_world_size()
+    mine = torch.tensor([solve_ms, gather_ms, 1e3 * elapsed_s], dtype=torch.float64, device=dev)
+    every = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    v = torch.stack(every).cpu().numpy()
+    return {"joined": world,
+            "solve_ms_min": round(float(v[:, 0].min()), 4), "solve_ms_max": round(float(v[:, 0].max()), 4),
+            "slowest_solve_rank": int(v[:, 0].argmax()),
+            "gather_ms_max": round(float(v[:, 1].max()), 4),
+            "timed_ms_min": round(float(v[:, 2].min()), 3), "timed_ms_max": round(float(v[:, 2].max()), 3),
+            "solve_ms_per_rank": [round(float(x), 4) for x in v[:, 0]],
+            "gather_ms_per_rank": [round(float(x), 4) for x in v[:, 1]]}
 
 
 def hook_main(a, hook, dist, world, rank, N, K, B, d):
@@ -278,8 +301,15 @@ def hook_main(a, hook, dist, world, rank, N, K, B, d):
     dev = torch.device("cpu")
     wl = make_workload(B, N, seed=1000 + rank, random_gait=a.random_gait)
     inputs = [torch.from_numpy(x) for x in wl.inputs]
-    sh = ShardedMPC(N, K, world * B, device=dev, y0=1.0, solve_fn=load_solve_hook(hook)(N, K))
-    elapsed, u0_last = run_timed(sh, inputs, a, dist, world, dev)
+    solve = load_solve_hook(hook)(N, K)
+    sh = ShardedMPC(N, K, world * B, device=dev, y0=1.0, solve_fn=solve)
+    elapsed, u0_last, own = run_timed(sh, inputs, a, dist, world, dev)
+    t1 = time.perf_counter()
+    x = solve(inputs)
+    solve_ms = 1e3 * (time.perf_counter() - t1)
+    t1 = time.perf_counter()
+    sh.gather_u0(x[:, 12 * N:12 * N + 12])
+    ranks = rank_spread(dist, dev, solve_ms, 1e3 * (time.perf_counter() - t1), own)
     if rank == 0:
         if a.dump_u0:
             np.save(a.dump_u0, u0_last.numpy())
@@ -290,7 +320,8 @@ def hook_main(a, hook, dist, world, rank, N, K, B, d):
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"CPU solve hook {hook} (launcher test; not a GPU measurement)",
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "pdipm_iters": K,
-                       "parallelism": f"dp{world}" + (" (u0 all_gather over gloo)" if world > 1 else "")}})
+                       "parallelism": f"dp{world}" + (" (u0 all_gather over gloo)" if world > 1 else "")},
+            "ranks": ranks})
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
@@ -322,6 +353,10 @@ def dropin_leg(inputs, N: int, B: int, reps: int) -> dict:
     out = {}
     xs = {}
     for name, lean in (("literal", False), ("lean", True)):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
         sched = ReferenceQPSchedule(N, B, lean=lean)
         xs[name] = sched.run(inputs)  # warm: library load, attribute setup
         torch.cuda.synchronize()
@@ -330,6 +365,9 @@ def dropin_leg(inputs, N: int, B: int, reps: int) -> dict:
             sched.run(inputs)
         torch.cuda.synchronize()
         out[f"{name}_ms"] = round(1e3 * (time.perf_counter() - t0) / max(2, reps // 2), 4)
+        # device memory the leg allocated at its peak (CusadiFunction buffers + the schedule's
+        # temporaries), above what was allocated before it
+        out[f"{name}_peak_mb"] = round((torch.cuda.max_memory_allocated() - base) / 2**20, 1)
         del sched
     bufs = solver.MPCSolveBuffers.allocate(N, B, inputs[0].device)
     out["fused_k20_ms"] = round(event_time_ms(lambda: solver.mpc_solve(inputs, N, 20, 1.0, buffers=bufs), reps), 4)
@@ -339,18 +377,53 @@ def dropin_leg(inputs, N: int, B: int, reps: int) -> dict:
     out["note"] = ("MPCControllerCusadi.run's QP schedule (INTEGRATION.md option A): 1 former + 4 x 5-iteration "
                    "evaluate, blocking, through CusadiFunction; 'literal' keeps the reference's dense "
                    "getDenseOutput rebuilds, bmm init and clones, 'lean' feeds the sparse outputs back; "
-                   "fused_k20 = the same 20 Newton iterations as one srbd_mpc_solve_fused launch")
+                   "fused_k20 = the same 20 Newton iterations as one srbd_mpc_solve_fused launch; *_peak_mb = the "
+                   "leg's peak device memory above the bench's own (CusadiFunction.outputs_dense is allocated "
+                   "only when read, so the never-written dense outputs hold no HBM)")
     return out
+
+
+C3_N, C3_B, C3_K, C3_SAMPLE = 20, 4096, 10, 64
+
+
+def config3_leg(dev, reps: int) -> dict:
+    """BASELINE config 3 (batch 4096, horizon N = 20, 10 iterations, one GPU): the fused step kernel
+    (mpc_step_reg_kernel<20>: former + cold PDIPM, one launch) timed with HIP events on the launch
+    stream, after the timed steps (steady clocks), and its FP64 roofline fraction (SURVEY 8d flops)."""
+    wl = make_workload(C3_B, C3_N, seed=3000)
+    inputs = [torch.from_numpy(x).to(dev) for x in wl.inputs]
+    bufs = solver.MPCSolveBuffers.allocate(C3_N, C3_B, dev)
+    ms = event_time_ms(lambda: solver.mpc_solve(inputs, C3_N, C3_K, 1.0, buffers=bufs), max(reps, 20), warm=3)
+    flops = WORK[C3_N]["flops_per_iter"] * C3_K * C3_B
+    idx = np.arange(0, C3_B, C3_B // C3_SAMPLE)
+    return {"workload": f"batch {C3_B}, N={C3_N}, {C3_K} PDIPM iters, standing gait (BASELINE configs[2])",
+            "kernel": solver_kernel_name(C3_N), "kernel_ms": round(ms, 4),
+            "solves_per_s": round(C3_B / (ms * 1e-3), 1),
+            "frac": round(flops / (ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 6),
+            "_wl": [x[idx] for x in wl.inputs], "_x": bufs.outputs[0][idx].cpu().numpy()}
+
+
+def config3_parity(sample_inputs, x, threads: int) -> dict:
+    """u0 of the config-3 sample (64 strided envs of the timed batch) vs the oracle (checker only)."""
+    from oracle import oracle
+    ref = oracle.mpc_solve(C3_N, C3_K, sample_inputs, y0=1.0, nthreads=threads)[0]
+    ug, ur = x[:, 12 * C3_N:12 * C3_N + 12], ref[:, 12 * C3_N:12 * C3_N + 12]
+    du = np.abs(ug - ur)
+    return {"max_rel_du": float((du.max(axis=1) / np.abs(ur).max(axis=1)).max()),
+            "max_rel_x": float((np.abs(x - ref).max(axis=1) / np.abs(ref).max(axis=1)).max()),
+            "parity_envs": int(x.shape[0])}
 
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
     env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and a.gpus > 1:
+    if env_world is None and a.gpus is not None and a.gpus > 1:
         sys.exit(launch_ranks(a, argv))  # this process only starts and joins the ranks
     _claim_stdout()
     world = int(env_world or "1")
+    if a.gpus is None:  # torchrun --nproc-per-node N bench.py: the launcher's WORLD_SIZE decides
+        a.gpus = world
     if a.gpus < 1 or world != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} ranks were launched", file=sys.stderr)
         sys.exit(2)
@@ -367,7 +440,7 @@ def main(argv=None):
     if not hook and local >= torch.cuda.device_count():
         print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible", file=sys.stderr)
         sys.exit(2)
-    if world > 1:
+    if env_world is not None:  # under a launcher (ours or torch.distributed.run): a process group, even of one
         import torch.distributed as dist_mod
         dist = dist_mod
         if backend == "nccl":
@@ -403,7 +476,7 @@ def main(argv=None):
     ms_fused = event_time_ms(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), a.kernel_reps)
     del pd_out
 
-    elapsed, u0_last = run_timed(sh, inputs, a, dist, world, dev)
+    elapsed, u0_last, own_elapsed = run_timed(sh, inputs, a, dist, world, dev)
     ms_step = 1e3 * elapsed / a.steps
     value = world * B * a.steps / elapsed
     if rank == 0 and a.dump_u0:
@@ -442,7 +515,13 @@ def main(argv=None):
     if dist is not None:
         u0 = bufs.outputs[0][:, 12 * N:12 * N + 12]
         ms_gather = event_time_ms(lambda: sh.gather_u0(u0), a.kernel_reps)
-
+    ranks = rank_spread(dist, dev if backend == "nccl" else torch.device("cpu"), ms_fused,
+                        ms_gather or 0.0, own_elapsed)
+    # BASELINE config 3 (batch 4096, N = 20, K = 10) under the driver's clock: its fused step kernel
+    # timed with HIP events (+ a 64-env oracle parity sample in the CPU leg below)
+    c3 = None
+    if rank == 0 and (N, K) == (10, 10) and not a.no_config3:
+        c3 = config3_leg(dev, a.kernel_reps)
     w = WORK.get(N)
     roofline = None
     if w is not None:
@@ -570,6 +649,11 @@ def main(argv=None):
         parity = {"max_abs_du": float(du.max()),
                   "max_rel_du": float((du.max(axis=1) / np.abs(ur).max(axis=1)).max()),
                   "envs": sample, "vs": "oracle (CPU restatement; CasADi unavailable: parity unpinned)"}
+        if c3 is not None:
+            c3.update(config3_parity(c3.pop("_wl"), c3.pop("_x"), threads))
+    if c3 is not None:
+        c3.pop("_wl", None)
+        c3.pop("_x", None)
     if dist is not None:
         dist.barrier()  # the other ranks wait for rank 0's CPU leg before tearing down
 
@@ -600,6 +684,8 @@ def main(argv=None):
             # the reference caller's own schedule through the CusADi-ABI drop-ins (INTEGRATION.md option A)
             "dropin_step_ms": None if dropin is None else dropin["literal_ms"],
             "dropin_step": dropin,
+            "config3": c3,  # BASELINE configs[2]: batch 4096, N = 20, 10 iterations, one GPU
+            "ranks": ranks,  # N > 1: per-rank solve / gather / timed-region spread
         }
         emit(line)
     if dist is not None:

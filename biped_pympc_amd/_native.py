@@ -67,6 +67,16 @@ def lib() -> ctypes.CDLL:
                                 _c_dp, ctypes.c_void_p]
     L.srbd_prepare_device.restype = ctypes.c_int
     L.srbd_prepare_device.argtypes = []
+    L.srbd_release_device.restype = ctypes.c_int
+    L.srbd_release_device.argtypes = []
+    L.srbd_set_scratch_slots.restype = ctypes.c_int
+    L.srbd_set_scratch_slots.argtypes = [ctypes.c_int]
+    L.srbd_scratch_pool_bytes.restype = ctypes.c_size_t
+    L.srbd_scratch_pool_bytes.argtypes = []
+    L.srbd_scratch_pool_slots.restype = ctypes.c_int
+    L.srbd_scratch_pool_slots.argtypes = []
+    L.srbd_scratch_slot_bytes.restype = ctypes.c_size_t
+    L.srbd_scratch_slot_bytes.argtypes = []
     L.srbd_evaluate_qp_former.restype = ctypes.c_float
     L.srbd_evaluate_qp_former.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int]
@@ -195,6 +205,22 @@ def prepare_device() -> None:
     Call it before capturing a solver call in a HIP graph (the first solver call on a device
     allocates it otherwise, which a capture does not allow)."""
     check(lib().srbd_prepare_device(), "srbd_prepare_device")
+
+
+def release_device() -> None:
+    """srbd_release_device(): free the current device's pool (device synchronised first)."""
+    check(lib().srbd_release_device(), "srbd_release_device")
+
+
+def set_scratch_slots(slots: int) -> None:
+    """srbd_set_scratch_slots(slots): cap the current device's pool (0 = one slot per resident
+    workgroup, the default)."""
+    check(lib().srbd_set_scratch_slots(int(slots)), "srbd_set_scratch_slots")
+
+
+def scratch_pool() -> dict:
+    """The current device's pool: {"slots", "bytes"} (0 / 0 before it is allocated)."""
+    return {"slots": int(lib().srbd_scratch_pool_slots()), "bytes": int(lib().srbd_scratch_pool_bytes())}
 
 
 def last_error() -> str:

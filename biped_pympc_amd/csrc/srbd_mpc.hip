@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -93,11 +94,15 @@ int launch_former(const srbd::FormerArgs& a, hipStream_t s) {
 }
 
 // The per-device scratch pool of the stage-invariant solver kernels (pdipm.hpp
-// pdipm_general_scratch): CUs x kMaxQpsPerCu slots of general_slot_doubles() (2048 slots, ~327 MB
-// of the 288 GB on an MI355X) and their lock words, one per 128-byte line, allocated on the first
-// stage-invariant solver call on a device (or srbd_prepare_device) and kept for the process. With a
-// slot for every resident workgroup no fallback solve waits for another: a batch of QPs that are all
-// not stage-invariant runs at the general solve's rate instead of queueing on a few slots.
+// pdipm_general_scratch): CUs x kMaxQpsPerCu slots of general_slot_doubles() (2048 slots of
+// srbd_scratch_slot_bytes() = 162,000 B: 332 MB of the 288 GB on an MI355X) and their lock words, one
+// per 128-byte line, allocated on the first stage-invariant solver call on a device (or
+// srbd_prepare_device) and kept until srbd_release_device. With a slot for every resident workgroup
+// no fallback solve waits for another: a batch of QPs that are all not stage-invariant runs at the
+// general solve's rate instead of queueing on a few slots. srbd_set_scratch_slots (or the
+// SRBD_SCRATCH_SLOTS environment variable, read when the pool is allocated) caps the slot count, for
+// processes that share a GPU: a fallback QP that finds every slot taken waits for one (the holders are
+// resident workgroups, so they finish), which is correct at any count >= 1, only slower.
 struct ScratchPool {
   double* buf = nullptr;
   int* locks = nullptr;
@@ -116,7 +121,28 @@ int general_slot_doubles() {
   return s;
 }
 srbd::PerDevice<ScratchPool> g_scratch;
+srbd::PerDevice<int> g_scratch_cap;  // srbd_set_scratch_slots per device; 0 = default
 std::mutex g_scratch_mu;
+
+// slots of a new pool on device `dev` with `cus` compute units
+int pool_slots(int dev, int cus) {
+  const int* capp = g_scratch_cap.at(dev);
+  int cap = capp ? *capp : 0;
+  if (cap <= 0)
+    if (const char* env = std::getenv("SRBD_SCRATCH_SLOTS")) cap = std::atoi(env);
+  return cap > 0 ? std::min(cap, 1 << 16) : cus * kMaxQpsPerCu;
+}
+
+// frees the pool of `pool` after the device has drained (g_scratch_mu held)
+int release_pool(ScratchPool* pool) {
+  if (!pool || !pool->buf) return 0;
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return set_error((int)e, "srbd_release_device: device synchronisation");
+  (void)hipFree(pool->buf);
+  (void)hipFree(pool->locks);
+  *pool = ScratchPool{};
+  return 0;
+}
 
 // the current device's pool, allocated on first use (`s`: the stream of the calling launch, checked for
 // capture; null from srbd_prepare_device)
@@ -139,7 +165,7 @@ ScratchPool* scratch_pool(hipStream_t s, bool check_capture, int& rc) {
     const size_t per_slot = (size_t)general_slot_doubles();
     int cus = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int slots = (e == hipSuccess && cus > 0 ? cus : 256) * kMaxQpsPerCu;
+    const int slots = pool_slots(dev, e == hipSuccess && cus > 0 ? cus : 256);
     const size_t lock_ints = (size_t)slots * srbd::kLockStride;
     double* buf = nullptr;
     int* locks = nullptr;
@@ -283,6 +309,44 @@ int srbd_prepare_device(void) {
   int rc = 0;
   return scratch_pool(nullptr, false, rc) ? 0 : rc;
 }
+
+int srbd_release_device(void) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  ScratchPool* pool = g_scratch.at(current_device());
+  if (!pool) return set_error((int)hipErrorInvalidDevice, "srbd_release_device: no current HIP device");
+  return release_pool(pool);
+}
+
+int srbd_set_scratch_slots(int slots) {
+  if (slots < 0) return set_error(kErrInvalid, "srbd_set_scratch_slots: slots >= 0 (0 = one per resident workgroup)");
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  const int dev = current_device();
+  int* cap = g_scratch_cap.at(dev);
+  ScratchPool* pool = g_scratch.at(dev);
+  if (!cap || !pool) return set_error((int)hipErrorInvalidDevice, "srbd_set_scratch_slots: no current HIP device");
+  *cap = slots;
+  if (pool->buf) {  // re-sized on the next solver call (or srbd_prepare_device)
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (pool_slots(dev, cus) != pool->slots) return release_pool(pool);
+  }
+  return 0;
+}
+
+size_t srbd_scratch_pool_bytes(void) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  const ScratchPool* pool = g_scratch.at(current_device());
+  if (!pool || !pool->buf) return 0;
+  return sizeof(double) * (size_t)pool->stride * pool->slots + sizeof(int) * (size_t)pool->slots * srbd::kLockStride;
+}
+
+int srbd_scratch_pool_slots(void) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  const ScratchPool* pool = g_scratch.at(current_device());
+  return pool ? pool->slots : 0;
+}
+
+size_t srbd_scratch_slot_bytes(void) { return sizeof(double) * (size_t)general_slot_doubles(); }
 
 size_t srbd_mpc_workspace_doubles(int horizon, int batch) {
   if (!horizon_ok(horizon) || batch < 0) return 0;

@@ -9,7 +9,12 @@ deliberate:
   * a failing kernel raises ``RuntimeError`` with the library's message instead of the reference's
     ``exit(code)`` inside ``gpuErrchk`` (``generateCUDACode.py:106-112``);
   * the device pointer tables are refreshed with one host->device copy instead of one per element,
-    and ``getDenseOutput`` is one scatter kernel over a cached index map (same results).
+    and ``getDenseOutput`` is one scatter kernel over a cached index map (same results);
+  * ``outputs_dense`` is allocated lazily, entry by entry, when it is read: the reference allocates
+    a zeroed ``(B, size1, size2)`` tensor per output in ``_setup`` (``CusadiFunction.py:77-81``)
+    that nothing ever writes (``getDenseOutput`` returns a new tensor), which for ``qp_former`` at
+    B = 4096, N = 10 is 4.25 GB of HBM held for nothing. Reading ``outputs_dense[i]`` still gives
+    that zeroed tensor.
 As in the reference, the caller's tensors are used in place through ``data_ptr()`` and their
 strides are NOT consulted: pass contiguous ``(num_instances, nnz_in[i])`` FP64 CUDA tensors.
 """
@@ -23,6 +28,38 @@ import torch
 
 from biped_pympc_amd.build import LIB_DIR, build_dropin
 from biped_pympc_amd.controller import dense_scatter, inverse_index
+
+
+class _LazyDenseOutputs:
+    """``outputs_dense`` of a CusadiFunction: a sequence of zeroed ``(B, size1_out(i), size2_out(i))``
+    FP64 tensors, each allocated on its first read and then kept (as the reference's list is)."""
+
+    def __init__(self, fn, num_instances: int, device):
+        self._fn, self._B, self._device = fn, num_instances, device
+        self._cache = {}
+
+    def __len__(self):
+        return self._fn.n_out()
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        if i not in self._cache:
+            self._cache[i] = torch.zeros((self._B, self._fn.size1_out(i), self._fn.size2_out(i)),
+                                         device=self._device, dtype=torch.double)
+        return self._cache[i]
+
+    def __iter__(self):
+        return (self[k] for k in range(len(self)))
+
+    @property
+    def allocated(self) -> list[int]:
+        """Indices of the entries read so far (the others hold no device memory)."""
+        return sorted(self._cache)
 
 
 class CusadiFunction:
@@ -98,9 +135,7 @@ class CusadiFunction:
                                for i in range(fn.n_in())]
         self._output_tensors = [torch.zeros(B, fn.nnz_out(i), device=self._device, dtype=torch.double)
                                 for i in range(fn.n_out())]
-        self._output_tensors_dense = [torch.zeros((B, fn.size1_out(i), fn.size2_out(i)),
-                                                  device=self._device, dtype=torch.double)
-                                      for i in range(fn.n_out())]
+        self._output_tensors_dense = _LazyDenseOutputs(fn, B, self._device)
         self._work_tensor = torch.zeros((B, max(fn.sz_w(), 1)), device=self._device, dtype=torch.double)
         self._input_ptrs = torch.zeros(fn.n_in(), device=self._device, dtype=torch.int64)
         self._output_ptrs = torch.tensor([t.data_ptr() for t in self._output_tensors],

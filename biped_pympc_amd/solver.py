@@ -151,8 +151,8 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     Equivalent to the GPU caller's step (mpc_controller_cusadi.py:99-169) with the Newton
     iteration count as a runtime argument. Returns [x, s, z, y, residuals, mu].
     ``fused`` (default): one kernel forms the QP in registers / LDS and solves it
-    (``srbd_mpc_solve_fused``; the register kernels at N = 10 and 20, the LDS-resident step kernel at
-    other horizons): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to their
+    (``srbd_mpc_solve_fused``; the register-resident step kernel at every N in 2..32, the
+    LDS-resident step kernel at N = 1): no QP data reaches memory, unless ``keep_qp`` (then f, b, d go to their
     ``buffers.workspace`` slots); ``False`` runs the former and the solver as two kernels with the
     full QP in the workspace. Both give the same bits. ``status`` (int32 (B,), optional) receives
     the per-problem status word.

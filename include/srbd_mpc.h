@@ -81,7 +81,10 @@ int srbd_pdipm_ccs(int horizon, int n_iter, int batch, const double* const* inpu
  *   SRBD_STATUS_NONFINITE  a NaN / Inf in the returned x, s, z, y or mu
  *   SRBD_STATUS_STEP_FLOOR a combined-direction step length (primal or dual) at its 1e-12 floor in the
  *                          last iteration (the iterate is stalled at the boundary)
- *   SRBD_STATUS_FALLBACK   the QP was not stage-invariant and took the general solve
+ *   SRBD_STATUS_FALLBACK   the QP was not stage-invariant and a stage-invariant kernel (solver path
+ *                          "auto" or "lds") solved it by its in-launch general fallback; set only there:
+ *                          under the "general" path (srbd_set_solver_path(1)) every QP takes the general
+ *                          kernel and this bit stays clear
  * Written by the *_ex entry points when status != NULL (device memory, batch ints). */
 #define SRBD_STATUS_NONFINITE 1
 #define SRBD_STATUS_STEP_FLOOR 2
@@ -132,13 +135,33 @@ int srbd_set_solver_path(int path);
 int srbd_get_solver_path(void);
 
 /* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the
- * stage-invariant kernels (one slot per resident workgroup -- 2048 on an MI355X, ~324 MB of HBM -- plus their lock words) -- on the current HIP
+ * stage-invariant kernels (one slot per resident workgroup -- 2048 on an MI355X of
+ * srbd_scratch_slot_bytes() = 162,000 B each: 332 MB of HBM per process and device, lock words
+ * included) -- on the current HIP
  * device, synchronising it. Optional: the first srbd_pdipm* / srbd_mpc_solve* / evaluate call on a
  * device does the same, but that first call must then not be made inside a stream capture (it returns
  * an error there): call this, or make one ordinary call, before capturing a graph. Returns 0 or an
  * error code. (The pool's lock words are released by the workgroups that take them; a kernel that
  * faults leaves the HIP context unusable anyway.) */
 int srbd_prepare_device(void);
+
+/* Frees the current device's scratch pool after synchronising the device (the next solver call, or
+ * srbd_prepare_device, allocates it again). Graphs captured before still hold the old pool's address:
+ * do not replay them afterwards. Returns 0 or an error code. */
+int srbd_release_device(void);
+
+/* Caps the current device's pool at `slots` (>= 1; 0 = the default, one per resident workgroup) for
+ * processes that share a GPU; the environment variable SRBD_SCRATCH_SLOTS does the same when no cap
+ * is set. Any count >= 1 is correct: a QP that is not stage-invariant and finds every slot taken
+ * waits for one. A pool of another size is released (device synchronised) and re-allocated on the
+ * next call. */
+int srbd_set_scratch_slots(int slots);
+
+/* Bytes / slots of the current device's pool (0 before it is allocated), and the bytes of one slot
+ * (host-only: no device needed). */
+size_t srbd_scratch_pool_bytes(void);
+int srbd_scratch_pool_slots(void);
+size_t srbd_scratch_slot_bytes(void);
 
 /* Host-only introspection: rebuild the CCS pattern of H (which = 0), A (1) or G (2) from the very
  * offset maps the kernels use to address A_val/G_val. colptr has 24*horizon+1 entries, rowind nnz.

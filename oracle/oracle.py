@@ -83,6 +83,10 @@ def qp_former(N: int, inputs, B: int | None = None, nthreads: int = 0):
     return [o[0] for o in outs] if single else outs
 
 
+# status bit the oracle alone sets: its sparse LDL^T met a zero pivot (srbd_oracle.c ORACLE_STATUS_LDL_FAIL)
+STATUS_LDL_FAIL = 8
+
+
 def _status_arg(status):
     return None if status is None else status.ctypes.data_as(_I32P)
 
@@ -90,7 +94,7 @@ def _status_arg(status):
 def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0, status: np.ndarray | None = None):
     """inputs: Q_val, G_val, A_val, f, h, b, x, s, z, y as (B, nnz). Returns x, s, z, y, res(4), mu(1).
     status: an int32 (B,) array receiving the per-problem status word (srbd_oracle.c); with it a
-    failed factorisation is reported there instead of raising."""
+    failed factorisation is reported there (STATUS_LDL_FAIL) instead of raising."""
     register(N)
     d = layout.Dims(N)
     single = np.asarray(inputs[0]).ndim == 1

@@ -549,7 +549,10 @@ static double step_length(int m, const double *v, const double *dv) {
  * computed here with the same definition as the HIP kernels so tests can compare them):
  * bit 0 -- a non-finite value in the returned x, s, z, y or mu; bit 1 -- a combined-direction step
  * length (primal or dual) at its 1e-12 floor (sparse_pdipm_solver.py:501-502) in the last iteration.
- * (Bit 2, "solved by the general fallback", exists only on the GPU.) */
+ * (Bit 2, "solved by the general fallback", exists only on the GPU.) Bit 3 is the oracle's own: its
+ * sparse LDL^T met a zero pivot in some iteration (the batch entry points then return 0 and report
+ * the failure only here), so a test comparing GPU and oracle words sees an oracle that failed. */
+#define ORACLE_STATUS_LDL_FAIL 8
 static int nonfinite(const double *v, int n) {
   for (int i = 0; i < n; ++i)
     if (!isfinite(v[i])) return 1;
@@ -672,6 +675,7 @@ int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const
   out[5][0] = mu_new;
   if (status && (nonfinite(x, nz) || nonfinite(s, m) || nonfinite(z, m) || nonfinite(y, p) || !isfinite(mu_new)))
     *status |= 1;
+  if (status && rc) *status |= ORACLE_STATUS_LDL_FAIL;
   free(x); free(s); free(z); free(y);
   free(w.Kx); free(w.Lx); free(w.Li); free(w.D); free(w.Y); free(w.Lnz); free(w.Pattern); free(w.Flag);
   free(rx); free(rs); free(re); free(tmp); free(sa); free(sc); free(Gx); free(sinv);

@@ -5,6 +5,9 @@ srbd_oracle_N{10,20}.npz -- named inputs and the oracle's qp_former + PDIPM outp
       env 0: demo point of srbd_constraints.py:244-282 (dt 0.04, m 13.5, mu 0.5, R = I, ...)
       env 1: demo point of generate_solver_function.py:19-58 (its Q/R weights)
       env 2-3: SURVEY 8d synthetic robots (standing gait), env 4-5: randomized gait + residuals.
+    Solver outputs K{K}_* start from the GPU caller's init (y0 = 1, mpc_controller_cusadi.py:138-141);
+    Y0_K{K}_* from the reference CPU path's init (y0 = 0, mpc_controller_casadi.py:182-199,
+    sparse_pdipm_solver.py:537-558), same x = 0, s = max(d, 1), z = 1.
     The reference itself cannot produce these (CasADi absent): parity unpinned.
 gait_reference.npz -- contact tables from the REFERENCE GaitGenerator.mpc_gait, imported
     standalone from /root/reference (gait_generator.py needs only torch), for the device-side
@@ -76,11 +79,12 @@ def main():
         H, f, A, b, G, d = oracle.qp_former(N, inputs)
         data = {f"in{k}": v for k, v in enumerate(inputs)}
         data.update(H=H, f=f, A=A, b=b, G=G, d=d)
-        x, s, z, y = solver_init(d, N, y0=1.0)
-        for K in ITERS:
-            out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, z, y])
-            for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
-                data[f"K{K}_{name}"] = v
+        for y0, prefix in ((1.0, ""), (0.0, "Y0_")):
+            x, s, z, y = solver_init(d, N, y0=y0)
+            for K in ITERS:
+                out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, z, y])
+                for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
+                    data[f"{prefix}K{K}_{name}"] = v
         np.savez_compressed(os.path.join(OUT, f"srbd_oracle_N{N}.npz"), **data)
         print("wrote", f"srbd_oracle_N{N}.npz")
     gg = "/root/reference/biped_pympc/core/gait/gait_generator.py"

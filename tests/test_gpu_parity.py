@@ -110,6 +110,45 @@ def test_runtime_horizon_solver_matches_oracle(N, K, path):
     assert np.all(np.isfinite(out[5].cpu().numpy()))  # no fallback sentinel left behind
 
 
+@pytest.mark.parametrize("path", ["auto", "lds", "general"])
+@pytest.mark.parametrize("K", [5, 20])
+@pytest.mark.parametrize("N", [1, 10, 20, 32])
+def test_cpu_path_dual_init_y0_zero(N, K, path):
+    """The reference CPU path's iterate init -- x = 0, s = max(d, 1), z = 1 and y = 0
+    (mpc_controller_casadi.py:182-199 via initialize_pdipm_variables, sparse_pdipm_solver.py:537-558;
+    the GPU caller uses y = 1, mpc_controller_cusadi.py:141) -- on the HIP path:
+    the cold-started solver (srbd_pdipm_cold, y0 = 0) and the fused former + solve
+    (srbd_mpc_solve_fused, y0 = 0) vs the oracle started the same way, every env, under every solver
+    path, at K = 5 (BASELINE config 1) and K = 20 (the CPU path's MAX_ITER, mpc_controller_casadi.py:31).
+    Per env: the SOLVER_CASES tolerance, or 4x that env's FP64 floor between the two CPU
+    restatements where that is higher (tests/golden/make_y0_floor.py: at N = 1, K = 20 one env's z
+    differs by 5.8e-4 between them)."""
+    from biped_pympc_amd import _native
+    B = 48
+    wl = make_workload(B, N, seed=300 + N, random_gait=True, residuals=True)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    ins = [H, G, A, f, d, b, *solver_init(d, N, y0=0.0)]
+    assert not ins[9].any()
+    ref = oracle.pdipm(N, K, ins)
+    ref_fused = oracle.mpc_solve(N, K, wl.inputs, y0=0.0)
+    with _native.solver_path(path):
+        cold = [t.clone() for t in solver.pdipm(_cuda(ins[:6]), None, N, K, y0=0.0)]
+        fused = solver.mpc_solve(_cuda(wl.inputs), N, K, y0=0.0)
+        torch.cuda.synchronize()
+    floor = np.load(os.path.join(GOLDEN, "dense_floor_y0.npz"))
+    tol = dict(SOLVER_CASES)[K]
+    for out, r in ((cold, ref), (fused, ref_fused)):
+        for k, v in enumerate("xszy"):
+            o = out[k].cpu().numpy()
+            assert np.all(np.isfinite(o))
+            err = rel_err_rows(o, r[k])
+            assert np.all(err <= np.maximum(tol, 4.0 * floor[f"N{N}_K{K}_{v}"])), (v, err.max())
+    # y = 0 really reached the kernels: the y = 1 start gives a different iterate
+    other = solver.pdipm(_cuda(ins[:6]), None, N, K, y0=1.0)
+    torch.cuda.synchronize()
+    assert not torch.equal(other[3], cold[3])
+
+
 def test_cold_start_matches_explicit_init():
     N, B, K = 10, 128, 10
     wl = make_workload(B, N, seed=7)
@@ -212,10 +251,11 @@ def test_mpc_solve_under_a_solver_path(N, path):
         assert e.max() <= dict(SOLVER_CASES)[K], (k, e.max())
 
 
-# (N, solver path, B, K): B = 600 QPs of which 400 are not stage-invariant contend for the 256 slots
-# of the in-launch fallback's scratch pool (pdipm.hpp pdipm_general_scratch); N = 20 / 25 / 32 run
-# multi-wave register QPs whose idle waves share the slot through LDS; "lds" runs the LDS-resident
-# kernel (pdipm_srbd_kernel) and its fallback
+# (N, solver path, B, K): B = 600 QPs of which 400 are not stage-invariant take the in-launch
+# fallback's scratch pool (pdipm.hpp pdipm_general_scratch: by default one slot per resident workgroup,
+# 2048 on an MI355X, so these do not contend -- test_mixed_batch_with_a_capped_pool makes them);
+# N = 20 / 25 / 32 run multi-wave register QPs whose waves share the slot through LDS; "lds" runs the
+# LDS-resident kernel (pdipm_srbd_kernel) and its fallback
 MIXED_CASES = [(10, "auto", 96, 10), (1, "auto", 600, 5), (5, "auto", 600, 5), (10, "auto", 600, 5),
                (20, "auto", 600, 5), (25, "auto", 600, 5), (32, "auto", 600, 5), (5, "lds", 600, 5),
                (20, "lds", 600, 5)]
@@ -223,8 +263,54 @@ MIXED_CASES = [(10, "auto", 96, 10), (1, "auto", 600, 5), (5, "auto", 600, 5), (
 
 @pytest.mark.parametrize("N,path,B,K", MIXED_CASES)
 def test_mixed_batch_routes_non_invariant_qps_to_the_general_kernel(N, path, B, K):
+    _mixed_batch_check(N, path, B, K)
+
+
+@pytest.mark.parametrize("N,path,B,K", [(10, "auto", 600, 5), (20, "auto", 600, 5), (32, "auto", 600, 5),
+                                        (5, "lds", 600, 5)])
+def test_mixed_batch_with_a_capped_pool(N, path, B, K):
+    """srbd_set_scratch_slots(3): 400 fallback QPs queue on 3 slots -- the slot search (s_sleep, wrap
+    at n) and the lock hand-over between workgroups that reuse a slot -- with the same results."""
     from biped_pympc_amd import _native
-    wl = make_workload(B, N, seed=77)
+    _native.set_scratch_slots(3)
+    try:
+        _mixed_batch_check(N, path, B, K)
+        assert _native.scratch_pool()["slots"] == 3
+    finally:
+        _native.set_scratch_slots(0)
+
+
+def test_capped_pool_shared_by_two_streams():
+    """Two mixed batches in flight at once on two streams over one 3-slot pool: both match the
+    oracle (no slot is handed to two workgroups; the lock words serialise them)."""
+    from biped_pympc_amd import _native
+    _native.set_scratch_slots(3)
+    try:
+        cases = [_mixed_inputs(10, 600, seed) for seed in (91, 92)]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = []
+        torch.cuda.synchronize()
+        for (ins, _), st in zip(cases, streams):
+            with torch.cuda.stream(st):
+                outs.append(solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), 10, 5))
+        torch.cuda.synchronize()
+        for (ins, _), out in zip(cases, outs):
+            ref = oracle.pdipm(10, 5, ins)
+            for k in range(4):
+                e = rel_err_rows(out[k].cpu().numpy(), ref[k])
+                assert e.max() <= 1e-7, (k, e.max())
+        pool = _native.scratch_pool()
+        assert pool["slots"] == 3 and pool["bytes"] > 0
+        _native.release_device()
+        assert _native.scratch_pool() == {"slots": 0, "bytes": 0}
+    finally:
+        _native.set_scratch_slots(0)
+    _native.prepare_device()  # the default pool again, before any capture test
+    assert _native.scratch_pool()["slots"] >= 256
+
+
+def _mixed_inputs(N, B, seed=77):
+    wl = make_workload(B, N, seed=seed)
     H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
     A = A.copy()
     G = G.copy()
@@ -235,7 +321,12 @@ def test_mixed_batch_routes_non_invariant_qps_to_the_general_kernel(N, path, B, 
         A[::3, layout.Dims(N).nnz_A - 1] *= 1.0 + 1e-3  # (N = 1: an x-moment entry of u_0)
     G[1::3, 28 * min(N - 1, 5) + 6] *= 0.9  # and one stage's G entry in others
     x, s, z, y = solver_init(d, N)
-    ins = [H, G, A, f, d, b, x, s, z, y]
+    return [H, G, A, f, d, b, x, s, z, y], wl
+
+
+def _mixed_batch_check(N, path, B, K):
+    from biped_pympc_amd import _native
+    ins, _ = _mixed_inputs(N, B)
     ref = oracle.pdipm(N, K, ins)
     st = torch.full((B,), -1, dtype=torch.int32, device="cuda")
     with _native.solver_path(path):
@@ -294,6 +385,29 @@ def test_cusadi_dropin_random_inputs(fn_kind):
     dense = cf.getDenseOutput(2 if fn_kind == "qp_former" else 0).cpu().numpy()
     if fn_kind == "qp_former":
         assert np.allclose(dense, layout.to_dense(ref[2], *layout.ccs_A(N), (14 * N, 24 * N)), atol=1e-12)
+
+
+def test_cusadi_outputs_dense_allocated_only_when_read():
+    """CusadiFunction.outputs_dense holds no device memory until an entry is read; a read entry is
+    the reference's zeroed (B, size1, size2) tensor (CusadiFunction.py:77-81, never written there)
+    and stays the same tensor; evaluate / getDenseOutput allocate none of them."""
+    from biped_pympc_amd.cusadi import CusadiFunction, qp_former_function
+    N, B = 10, 512
+    fn = qp_former_function(N)
+    dense_bytes = sum(B * fn.size1_out(i) * fn.size2_out(i) * 8 for i in range(fn.n_out()))
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated()
+    cf = CusadiFunction(fn, B)
+    wl = make_workload(B, N, seed=12)
+    cf.evaluate(_cuda(wl.inputs))
+    cf.getDenseOutput(2)
+    torch.cuda.synchronize()
+    assert cf.outputs_dense.allocated == []
+    assert torch.cuda.memory_allocated() - before < dense_bytes / 4
+    h = cf.outputs_dense[0]
+    assert h.shape == (B, fn.size1_out(0), fn.size2_out(0)) and h.dtype == torch.float64
+    assert not h.any() and cf.outputs_dense[0] is h and cf.outputs_dense.allocated == [0]
+    assert len(cf.outputs_dense) == fn.n_out() and len(list(cf.outputs_dense)) == fn.n_out()
 
 
 def test_api_rejects_bad_buffers():
@@ -401,16 +515,18 @@ def test_golden_fixtures_on_the_hip_path(N):
     for name, o in zip("H f A b G d".split(), former):
         assert rel_err(o.cpu().numpy(), g[name]) <= 1e-12, name
     qp = _cuda([g["H"], g["G"], g["A"], g["f"], g["d"], g["b"]])
-    for K, tol in SOLVER_CASES:
-        cold = [t.clone() for t in solver.pdipm(qp, None, N, K, y0=1.0)]
-        fused = solver.mpc_solve(_cuda(inputs), N, K, y0=1.0)
-        torch.cuda.synchronize()
-        for k, name in enumerate(["x", "s", "z", "y"]):
-            ref = g[f"K{K}_{name}"]
-            for out in (cold, fused):
-                e = rel_err_rows(out[k].cpu().numpy(), ref)
-                assert e.max() <= tol, (K, name, e.max())
-        np.testing.assert_allclose(fused[5].cpu().numpy(), g[f"K{K}_mu"], rtol=1e-6)
+    # K{K}_*: the GPU caller's init y0 = 1; Y0_K{K}_*: the reference CPU path's y0 = 0
+    for y0, prefix in ((1.0, ""), (0.0, "Y0_")):
+        for K, tol in SOLVER_CASES:
+            cold = [t.clone() for t in solver.pdipm(qp, None, N, K, y0=y0)]
+            fused = solver.mpc_solve(_cuda(inputs), N, K, y0=y0)
+            torch.cuda.synchronize()
+            for k, name in enumerate(["x", "s", "z", "y"]):
+                ref = g[f"{prefix}K{K}_{name}"]
+                for out in (cold, fused):
+                    e = rel_err_rows(out[k].cpu().numpy(), ref)
+                    assert e.max() <= tol, (y0, K, name, e.max())
+            np.testing.assert_allclose(fused[5].cpu().numpy(), g[f"{prefix}K{K}_mu"], rtol=1e-6)
 
 
 @pytest.mark.parametrize("N", [10, 20, 5])

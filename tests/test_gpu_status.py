@@ -41,8 +41,8 @@ def test_status_clean_batch_is_zero_and_changes_nothing(N, path):
         assert torch.equal(a[k], b[k]), k
     ref_st = np.zeros(B, np.int32)
     oracle.mpc_solve(N, K, wl.inputs, y0=1.0, status=ref_st)
+    assert not ref_st.any()  # bits 0-1 and the oracle's own LDL-failure bit 3 all clear
     assert np.array_equal(st.cpu().numpy(), ref_st)
-    assert not ref_st.any()
 
 
 @pytest.mark.parametrize("N", [1, 10, 20])
@@ -60,6 +60,7 @@ def test_status_flags_planted_nan(N, path):
     ref_st = np.zeros(B, np.int32)
     oracle.mpc_solve(N, K, inputs, y0=1.0, status=ref_st)
     got = st.cpu().numpy()
+    assert not (np.delete(ref_st, [3, 7]) & oracle.STATUS_LDL_FAIL).any()  # the checker itself did not fail
     assert (ref_st[[3, 7]] & _native.STATUS_NONFINITE).all()
     assert np.array_equal(got & _native.STATUS_NONFINITE, ref_st & _native.STATUS_NONFINITE)
     assert not (np.delete(got, [3, 7])).any()
@@ -88,6 +89,7 @@ def test_status_flags_stalled_warm_start(N, path):
     with _native.solver_path(path):
         solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K, status=st)
     torch.cuda.synchronize()
+    assert not (ref_st & oracle.STATUS_LDL_FAIL).any()  # the checker's factorisation did not fail
     assert (ref_st[:B // 2] == _native.STATUS_STEP_FLOOR).all() and not ref_st[B // 2:].any()
     assert np.array_equal(st.cpu().numpy(), ref_st)
 

@@ -68,6 +68,10 @@ def test_abi_introspection():
         assert 0 < lds <= 160 * 1024
     assert L.srbd_solver_lds_bytes(0) == 0 and L.srbd_solver_lds_bytes(33) == 0
     assert L.srbd_mpc_workspace_doubles(10, 4096) == 4096 * 2256
+    # one fallback scratch slot: the general solve's working set at its largest horizon (host-only);
+    # 2048 of them (+ lock words) are the per-device pool INTEGRATION.md prices at 332 MB
+    assert L.srbd_scratch_slot_bytes() == 162000
+    assert L.srbd_set_scratch_slots(-1) != 0 and "slots >= 0" in _native.last_error()
 
 
 def test_bad_arguments_return_errors_without_touching_the_gpu():

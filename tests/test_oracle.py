@@ -30,11 +30,14 @@ def test_oracle_reproduces_golden(N):
     H, f, A, b, G, d = oracle.qp_former(N, inputs)
     for name, v in zip("HfAbGd", (H, f, A, b, G, d)):
         assert np.array_equal(v, z[name]), name
-    x, s, zz, y = solver_init(d, N)
-    for K in (1, 5, 10, 20):
-        out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, zz, y])
-        for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
-            assert rel_err(v, z[f"K{K}_{name}"]) < 1e-13, (K, name)
+    # y0 = 1: the GPU caller's init (mpc_controller_cusadi.py:141); y0 = 0: the reference CPU path's
+    # (mpc_controller_casadi.py:197, sparse_pdipm_solver.py:556)
+    for y0, prefix in ((1.0, ""), (0.0, "Y0_")):
+        x, s, zz, y = solver_init(d, N, y0=y0)
+        for K in (1, 5, 10, 20):
+            out = oracle.pdipm(N, K, [H, G, A, f, d, b, x, s, zz, y])
+            for name, v in zip(("x", "s", "z", "y", "res", "mu"), out):
+                assert rel_err(v, z[f"{prefix}K{K}_{name}"]) < 1e-13, (y0, K, name)
 
 
 @pytest.mark.parametrize("K", [1, 3, 5, 10])
@@ -154,3 +157,26 @@ def test_kkt_symbolic_stats():
 def test_rel_err_rows_helper():
     a = np.array([[1.0, 2.0], [3.0, 4.0]])
     assert np.all(rel_err_rows(a, a) == 0)
+
+
+def test_oracle_status_reports_its_own_ldl_failure():
+    """With a status array the batch entry points return 0 on a failed factorisation and report it
+    only in the word: bit 3 (oracle.STATUS_LDL_FAIL) must then be set, so a GPU-vs-oracle status
+    comparison can never pass on a checker that failed. A QP whose H + beta I, A and G are all zero
+    has exactly zero pivots on the x columns."""
+    N = 10
+    z, inputs = _golden(N)
+    H, f, A, b, G, d = (z[k].copy() for k in "HfAbGd")
+    x, s, zz, y = solver_init(d, N)
+    bad = [np.full_like(H, -oracle_beta()), np.zeros_like(G), np.zeros_like(A), f, d, b, x, s, zz, y]
+    st = np.zeros(H.shape[0], np.int32)
+    oracle.pdipm(N, 1, [a[:2] for a in bad], status=st[:2])
+    assert (st[:2] & oracle.STATUS_LDL_FAIL).all()
+    ok = np.zeros(H.shape[0], np.int32)
+    oracle.pdipm(N, 1, [H, G, A, f, d, b, x, s, zz, y], status=ok)
+    assert not (ok & oracle.STATUS_LDL_FAIL).any()
+
+
+def oracle_beta():
+    from oracle.pdipm_dense import BETA
+    return BETA
