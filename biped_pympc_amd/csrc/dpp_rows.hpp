@@ -127,7 +127,113 @@ __device__ __forceinline__ void gj_pivot(double (&Sr)[12], double& sc) {
   if constexpr (K < 11) gj_pivot<K + 1>(Sr, sc);
 }
 
+// The same sweep software-pipelined across pivots (bit-identical: every value is formed by the same
+// operations in the same order). Pivot k+1's element a_{k+1,k+1} is final as soon as pivot k has
+// updated column k+1, so that column's broadcast-FMA goes first; pivot k+1's broadcast and
+// v_rcp_f64 then issue before pivot k's other ten broadcast-FMAs, which cover their latency, and
+// the Newton step and t follow them. In the serial order every pivot waits on DPP -> rcp -> 2 FMA ->
+// mul after its predecessor's last FMA. Where a partner wave hides that latency (one-wave QPs, two
+// per SIMD) the split asm blocks cost more than they save (round 2: N = 10 +0.8 %); a two-wave QP's
+// chain runs alone on its SIMD (its partner there is another QP's idle wave), where it pays.
+#define SRBD_PIVOT1(K, a) asm("s_nop 1\n" SRBD_FMAC_BC("%0", "%0", "-%1", K) "s_nop 1\n" : "+v"(S[a]) : "v"(t))
+#define SRBD_FMAC10(K)                                                                              \
+  SRBD_FMAC_BC("%0", "%0", "-%10", K) SRBD_FMAC_BC("%1", "%1", "-%10", K) SRBD_FMAC_BC("%2", "%2", "-%10", K) \
+  SRBD_FMAC_BC("%3", "%3", "-%10", K) SRBD_FMAC_BC("%4", "%4", "-%10", K) SRBD_FMAC_BC("%5", "%5", "-%10", K) \
+  SRBD_FMAC_BC("%6", "%6", "-%10", K) SRBD_FMAC_BC("%7", "%7", "-%10", K) SRBD_FMAC_BC("%8", "%8", "-%10", K) \
+  SRBD_FMAC_BC("%9", "%9", "-%10", K)
+#define SRBD_PIVOT10(K, a, b, c, d, e, f, g, h, i, j)                                                \
+  asm("s_nop 1\n" SRBD_FMAC10(K) SRBD_ASM_TAIL                                                       \
+      : "+v"(S[a]), "+v"(S[b]), "+v"(S[c]), "+v"(S[d]), "+v"(S[e]), "+v"(S[f]), "+v"(S[g]), "+v"(S[h]), \
+        "+v"(S[i]), "+v"(S[j])                                                                     \
+      : "v"(t), "v"(y))
+// pivot k's update of column k + 1 alone (its trailing s_nop 1: the next pivot's broadcast reads it)
+__device__ __forceinline__ void pivot_update_next(double (&S)[12], double t, int k) {
+  switch (k) {
+    case 0: SRBD_PIVOT1(0, 1); break;
+    case 1: SRBD_PIVOT1(1, 2); break;
+    case 2: SRBD_PIVOT1(2, 3); break;
+    case 3: SRBD_PIVOT1(3, 4); break;
+    case 4: SRBD_PIVOT1(4, 5); break;
+    case 5: SRBD_PIVOT1(5, 6); break;
+    case 6: SRBD_PIVOT1(6, 7); break;
+    case 7: SRBD_PIVOT1(7, 8); break;
+    case 8: SRBD_PIVOT1(8, 9); break;
+    case 9: SRBD_PIVOT1(9, 10); break;
+    default: SRBD_PIVOT1(10, 11); break;
+  }
+}
+// ... and of the ten columns other than k, k + 1 (y, the next pivot's raw reciprocal, is an unused
+// operand: it pins the broadcast and v_rcp_f64 that produce it in front of the ten FMAs, which the
+// scheduler would otherwise sink behind them)
+__device__ __forceinline__ void pivot_update_rest(double (&S)[12], double t, double y, int k) {
+  switch (k) {
+    case 0: SRBD_PIVOT10(0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 1: SRBD_PIVOT10(1, 0, 3, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 2: SRBD_PIVOT10(2, 0, 1, 4, 5, 6, 7, 8, 9, 10, 11); break;
+    case 3: SRBD_PIVOT10(3, 0, 1, 2, 5, 6, 7, 8, 9, 10, 11); break;
+    case 4: SRBD_PIVOT10(4, 0, 1, 2, 3, 6, 7, 8, 9, 10, 11); break;
+    case 5: SRBD_PIVOT10(5, 0, 1, 2, 3, 4, 7, 8, 9, 10, 11); break;
+    case 6: SRBD_PIVOT10(6, 0, 1, 2, 3, 4, 5, 8, 9, 10, 11); break;
+    case 7: SRBD_PIVOT10(7, 0, 1, 2, 3, 4, 5, 6, 9, 10, 11); break;
+    case 8: SRBD_PIVOT10(8, 0, 1, 2, 3, 4, 5, 6, 7, 10, 11); break;
+    case 9: SRBD_PIVOT10(9, 0, 1, 2, 3, 4, 5, 6, 7, 8, 11); break;
+    default: SRBD_PIVOT10(10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9); break;
+  }
+}
+// pivot lanes of step K: a_KK <- 0 (so t = a_KK id is 0 there and their update is a no-op)
+template <int K>
+__device__ __forceinline__ void pivot_zero(double& x) {
+  uint64_t sv;
+  asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], 0\n\ts_mov_b64 exec, %[sv]"
+      : [x] "+v"(x), [sv] "=&s"(sv)
+      : [m] "n"(PivotLanes<K>::value));
+}
+// pivot lanes of step K after the update: a_KK <- -1, scale <- id
+template <int K>
+__device__ __forceinline__ void pivot_finish(double& x, double& sc, double id) {
+  uint64_t sv;
+  asm("s_and_saveexec_b64 %[sv], %[m]\n\tv_mov_b64 %[x], -1.0\n\tv_mov_b64 %[s], %[id]\n\ts_mov_b64 exec, %[sv]"
+      : [x] "+v"(x), [s] "+v"(sc), [sv] "=&s"(sv)
+      : [id] "v"(id), [m] "n"(PivotLanes<K>::value));
+}
+// step K of the pipelined sweep, entered with pivot K's reciprocal id and multiplier t formed
+template <int K>
+__device__ __forceinline__ void gj_pivot_swp(double (&Sr)[12], double& sc, double id, double t) {
+  if constexpr (K < 11) {
+    pivot_update_next(Sr, t, K);               // column K + 1 first: a_{K+1,K+1} is now final
+    const double pk = bc16(Sr[K + 1], K + 1);  // pivot K + 1's element ...
+    const double y = __builtin_amdgcn_rcp(pk);  // ... and its raw reciprocal, in flight while
+    pivot_update_rest(Sr, t, y, K);            // pivot K updates its ten other columns
+    Sr[K] = t;
+    pivot_finish<K>(Sr[K], sc, id);
+    pivot_zero<K + 1>(Sr[K + 1]);
+#ifdef SRBD_RCP_CUBIC
+    const double e = fma(-pk, y, 1.0);
+    const double idn = fma(y, fma(e, e, e), y);
+#else
+    const double idn = fma(y, fma(-pk, y, 1.0), y);  // rcp3's Newton step
+#endif
+    gj_pivot_swp<K + 1>(Sr, sc, idn, Sr[K + 1] * idn);
+  } else {
+    pivot_update(Sr, t, K);
+    Sr[K] = t;
+    pivot_finish<K>(Sr[K], sc, id);
+  }
+}
+// kSwp: the software-pipelined sweep (same bits)
+template <bool kSwp = false>
 __device__ __forceinline__ void inverse_rows12(double (&Sr)[12], double (&Dr)[12]) {
+  if constexpr (kSwp) {
+    double sc = 1.0;
+    const double pk = bc16(Sr[0], 0);
+    pivot_zero<0>(Sr[0]);
+    const double id = rcp3(pk);
+    gj_pivot_swp<0>(Sr, sc, id, Sr[0] * id);
+    const double nsc = -sc;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) Dr[j] = Sr[j] * nsc;
+    return;
+  }
   double sc = 1.0;
   gj_pivot<0>(Sr, sc);
   // the sweep leaves -(A^-1) (times the row scale): flip the sign while applying the scale

@@ -199,7 +199,7 @@ __device__ inline double ccs_gx(const double* Gv, int q, const double* xu) {
 struct SolverCtx {
   int N, nz, m, p, nd, lane;
   // nt: the threads a QP's row-parallel loops stride over (kGeneralThreads in the general kernel; in
-  // the fallback the calling kernel's threads per QP: 64, 128 or 192); RD: one partial per wave
+  // the fallback the calling kernel's threads per QP: 64, 128, 192 or 256); RD: one partial per wave
   int nt;
   double* RD;
   double *AV, *GV, *HV, *X, *S, *Z, *Y, *RX, *RS, *RE, *SI, *WD, *DI, *R2, *VV, *PH, *DV, *R1T, *TV,

@@ -26,16 +26,24 @@
 #ifndef SRBD_PHASE_ATTR
 #define SRBD_PHASE_ATTR  // diagnostic builds: __attribute__((noinline)) to read one phase ISA alone
 #endif
+#ifndef SRBD_SWP_INV
+#define SRBD_SWP_INV 0  // two-wave QPs invert their chain blocks by the software-pipelined sweep: measured slower, off
+#endif
+#ifndef SRBD_PIPE_FACTOR
+#define SRBD_PIPE_FACTOR 0  // stage-pipelined factorisation of two-wave QPs: built and measured slower, off
+#endif
 
 namespace srbd {
 
 // Threads per QP: one wave at N <= 10 (LDS and registers allow 2 QPs per SIMD); two waves beyond
 // (the LDS of a longer horizon allows 1 QP per SIMD, so a second wave of the SAME QP takes the other
-// half of every row-parallel phase and gives the SIMD a partner to hide latency behind). The block
-// chains and the per-stage tasks stay on wave 0.
-__host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : (N <= 21 ? 128 : 192); }
+// half of every row-parallel phase and gives the SIMD a partner to hide latency behind); three from
+// N = 22, four from N = 25 (2 QPs per CU by LDS either way: 8 waves per CU instead of 6, and two
+// inequality-row slots per lane instead of the three that spilled 6-30 VGPRs at 192 threads). The
+// block chains and the per-stage tasks stay on wave 0.
+__host__ __device__ constexpr int reg_tpb(int N) { return N <= 10 ? 64 : (N <= 21 ? 128 : (N <= 24 ? 192 : 256)); }
 // Horizons the register kernels are instantiated for: the equality-row slots need 6 N <= threads
-// per QP (one wave to N = 10, two to N = 21, three to N = 32) and the fused prologue's 17 inputs fit
+// per QP (one wave to N = 10, two to N = 21, three or four to N = 32) and the fused prologue's 17 inputs fit
 // the DV blocks from N = 2. N = 10 lives in srbd_mpc.hip, N = 20 in srbd_reg20.hip, the others in
 // srbd_regN.hip; N = 1 runs the LDS-resident kernels.
 __host__ __device__ constexpr bool reg_horizon(int N) { return N >= 2 && N <= 32; }
@@ -76,10 +84,16 @@ struct RegLayout {
                        QV = TV + nz, REm = QV + nx, DYm = REm + 2 * N,
                        RED = DYm + 2 * N,  // block reductions of a multi-wave QP: 2 slot sets
                        DMY = RED + (TPB > 64 ? 2 * (TPB / 64) : 0),  // sink of the invalid lanes' stores
-                       end = DMY + 2,
+                       end0 = DMY + 2,
                        // the fused prologue's FormerLds scratch from TV on (pads the short horizons)
-                       former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16),
-                       total = end > former ? end : former;
+                       former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16);
+  // The stage-pipelined factorisation of a two-wave QP (RegCtx::pipe_factor) keeps every stage's two
+  // inverted foot blocks Phi_f^-1 in PH (20 N doubles; the one-wave kernels use TV, dead at that
+  // point, as their scratch), where the QP still fits 4 per CU (160 KiB / 4): N <= 20.
+  static constexpr bool pipe = SRBD_PIPE_FACTOR && TPB == 128 &&
+                               8 * ((end0 + 20 * N) > former ? (end0 + 20 * N) : former) <= 40960;
+  static constexpr int PH = end0, end = end0 + (pipe ? 20 * N : 0), total = end > former ? end : former;
+  static_assert((PH & 1) == 0, "16-byte aligned foot blocks (read as double2)");
   // SE: the three equality-row register slots of RegCtx::erow (dynamics rows {0,1,2,6,7,8} and
   // {3,4,5,9,10,11} of every stage, then the x-moment rows), whatever the horizon
   static constexpr int SI = (m + TPB - 1) / TPB, SE = 3, SX = (nx + TPB - 1) / TPB;
@@ -126,6 +140,15 @@ static __constant__ uint8_t c_dvslot[78] = {77, 58, 32, 73, 46, 5,  52, 54, 50, 
                                             29, 18, 78, 51, 19, 61, 42, 79, 41, 24, 33, 39, 70, 55, 2,  22,
                                             37, 40, 67, 27, 26, 68, 60, 66, 57, 36, 59, 1,  45, 74, 56, 0,
                                             63, 7,  11, 12, 72, 10, 35, 25, 4,  16, 34, 62, 38, 13};
+
+// The pipelined S_ii build's entry of each lane (RegCtx::pipe_factor): pass A, lanes 0..63: the 21
+// dense x dense entries (positions 0..20 of the class-sorted table c_tab.dvo), then the 43 sparse-index
+// entries of foot position 0 or 1 and the first 7 of position 2; pass B, lanes 0..13: the other 14
+// entries of position 2 (tests/test_layout.py checks the partition)
+constexpr uint8_t kPipeEntry[78] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                    16, 17, 18, 19, 20, 21, 22, 23, 26, 29, 30, 32, 33, 35, 36, 37, 39, 42, 43, 44, 45, 47, 49, 50, 54, 55, 56, 57, 58, 59, 60, 63, 64, 67, 70, 71, 72, 73, 74, 76, 77, 24, 25, 27, 28, 31, 34, 38, 40, 41, 46, 48, 51, 52, 53, 61, 62, 65, 66, 68, 69, 75};
+static __constant__ uint8_t c_pipe_entry[78] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                                16, 17, 18, 19, 20, 21, 22, 23, 26, 29, 30, 32, 33, 35, 36, 37, 39, 42, 43, 44, 45, 47, 49, 50, 54, 55, 56, 57, 58, 59, 60, 63, 64, 67, 70, 71, 72, 73, 74, 76, 77, 24, 25, 27, 28, 31, 34, 38, 40, 41, 46, 48, 51, 52, 53, 61, 62, 65, 66, 68, 69, 75};
 
 // Byte offset, inside a step's block pair, of element (row r, column c) of chain lane l (group
 // g = l >> 4, row r = min(l & 15, 11), both in the group's coordinates): packed-lower slot of
@@ -402,10 +425,37 @@ struct RegCtx {
     }
   }
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
+  // Stage-pipelined factorisation (two-wave QPs, RegLayout::pipe): wave 1 forms the stage blocks and
+  // the dual right-hand side in the order the chain consumes them while wave 0 runs the chain, and
+  // the per-stage tasks (foot blocks of Phi_u, the scalar u columns) live on wave 1's lanes: FB is
+  // their first lane (task fl = lane - FB)
+  static constexpr bool kPipe = Lo::pipe;
+  // the chain's 12x12 block inverses by the software-pipelined sweep (inverse_rows12<true>), tried for
+  // two-wave QPs on the premise that their chain wave runs alone on its SIMD (profiles/r05/simd_probe.txt:
+  // its SIMD partner is another QP's second wave); measured +2.1 % at N = 20 (n20_pipeline.txt): off
+  static constexpr bool kSwpInv = SRBD_SWP_INV && TPB == 128;
+  static constexpr int FB = kPipe ? 64 : 0;
   static constexpr int kFactorUnroll = T + 1;  // chains fully unrolled (N = 20: -4.7 % vs rolled)
   double* L;
   int lane;
-  const double *fg, *hg, *bg;
+  // The CCS kernel's f, h, b rows of this env, addressed from the kernel's own argument (kernarg
+  // segment: scalar loads) at each use: a 64-bit row pointer held across the Newton loop is what the
+  // N = 21 kernel spilled (a scratch reload per iteration). Unused by the fused kernel (kFReg).
+  int env_ = 0;
+  // the pipelined S_ii build's two entries of this lane (pipe_factor), looked up once per solve:
+  // rows / columns of the pass-A and pass-B entries and their DV slots, 4 + 4 + 4 + 4 + 7 + 7 bits
+  int pipe_ix = 0;
+  __device__ void pipe_prep() {
+    const int lw = lane & 63;
+    const int ka = c_pipe_entry[lw], kb = c_pipe_entry[64 + (lw < 14 ? lw : 0)];
+    const int rca = c_tab.dvo[ka], rcb = c_tab.dvo[kb];
+    const int ra = rca & 15, ca = rca >> 4, rb = rcb & 15, cb = rcb >> 4;
+    const int sla = c_dvslot[ra * (ra + 1) / 2 + ca], slb = c_dvslot[rb * (rb + 1) / 2 + cb];
+    pipe_ix = ra | (ca << 4) | (rb << 8) | (cb << 12) | (sla << 16) | (slb << 23) | ((ka < 21) << 30);
+  }
+  __device__ const double* fg() const { return solver_in(kernel_args(), 3) + (size_t)env_ * nz; }
+  __device__ const double* hg() const { return solver_in(kernel_args(), 4) + (size_t)env_ * m; }
+  __device__ const double* bg() const { return solver_in(kernel_args(), 5) + (size_t)env_ * p; }
   // this lane's entries of f (x and u columns), b and h, held in registers for the whole solve:
   // set once (loaded, or as the fused kernel computes them), never re-read from memory
   double fxr[SX], fur[SX], bvr[SE], hvr[SI];
@@ -413,20 +463,27 @@ struct RegCtx {
 #pragma unroll
     for (int t = 0; t < (kFReg ? SX : 1); ++t) {
       const int c = min(lane + TPB * t, nx - 1);
-      fxr[t] = fg[c];
-      fur[t] = fg[nx + c];
+      fxr[t] = fg()[c];
+      fur[t] = fg()[nx + c];
     }
 #pragma unroll
     for (int t = 0; t < (kFReg ? SE : 2); ++t) {
       const ERow q = erow(lane, t);
-      bvr[t] = bg[q.valid ? q.e : 0];
+      bvr[t] = bg()[q.valid ? q.e : 0];
     }
 #pragma unroll
-    for (int t = 0; t < (kFReg ? SI : SI - 1); ++t) hvr[t] = hg[min(lane + TPB * t, m - 1)];
+    for (int t = 0; t < (kFReg ? SI : SI - 1); ++t) hvr[t] = hg()[min(lane + TPB * t, m - 1)];
   }
   // h of slot t (the CCS kernel re-reads its last slot from memory, see kFReg)
-  __device__ double hval(int t, int q) const { return (kFReg || t < SI - 1) ? hvr[t] : hg[q]; }
-  double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
+  __device__ double hval(int t, int q) const { return (kFReg || t < SI - 1) ? hvr[t] : hg()[q]; }
+  // ph: this foot-task lane's inverted foot block; the pipelined kernels re-read it from PH instead
+  // (20 VGPRs held across the Newton loop by every lane of both waves would spill the N = 20 kernel)
+  double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[kPipe ? 1 : 10];
+  // element e of foot task fl's inverted block (packed lower, sym_idx order)
+  __device__ void load_ph(int fl, double (&p)[10]) const {
+#pragma unroll
+    for (int e = 0; e < 10; ++e) p[e] = kPipe ? at(Lo::PH)[20 * (fl >> 1) + 10 * (fl & 1) + e] : ph[kPipe ? 0 : e];
+  }
   double e3r[SI];  // the affine refinement's row-3 residuals (degenerate iterations only)
   PROF_DECL
 
@@ -513,7 +570,7 @@ struct RegCtx {
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
         const int k = div12(c) + 1, j = c - m24(k - 1, 12);
-        const double v = Hu[12 + j] * X[c] + ((kFReg || t == 0) ? fx[t] : fg[c]);
+        const double v = Hu[12 + j] * X[c] + ((kFReg || t == 0) ? fx[t] : fg()[c]);
         double ay = Pd[j] * Y[12 * (k - 1) + j];
         const double my = mcol(Mc, j, Y + 12 * (k < N ? k : N - 1));  // k = N: unused
         ay = fma(k < N ? 1.0 : 0.0, my, ay);
@@ -525,7 +582,7 @@ struct RegCtx {
       const int c = lane + TPB * t;
       if (full_slot(t, nx) || c < nx) {
         const int i = div12(c), j = c - m24(i, 12);
-        const double v = Hu[j] * X[nx + c] + ((kFReg || t == 0) ? fu[t] : fg[nx + c]);
+        const double v = Hu[j] * X[nx + c] + ((kFReg || t == 0) ? fu[t] : fg()[nx + c]);
         // G^T z on the foot columns and the x-moment terms on columns 6 / 9, formed in every lane
         // (clamped foot index) and selected
         const int fj = foot_of(j), f = fj >= 0 ? fj : 0;
@@ -551,7 +608,7 @@ struct RegCtx {
       const ERow q = erow(lane, 2);
       if (q.valid) {
         const int w = q.r;
-        re[2] = SG[6 + w] * X[nx + 12 * q.i + (w ? 9 : 6)] - (kFReg ? bv[2] : bg[q.e]);
+        re[2] = SG[6 + w] * X[nx + 12 * q.i + (w ? 9 : 6)] - (kFReg ? bv[2] : bg()[q.e]);
         REm[q.e - nx] = re[2];
       }
     }
@@ -562,7 +619,7 @@ struct RegCtx {
       if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q >> 4, k = q & 15;
         const double v = grow4(Gf, k, X + nx + m24(i, 12));
-        rs[t] = (v + s[t]) - ((kFReg || t < SI - 1) ? hv[t] : hg[q]);
+        rs[t] = (v + s[t]) - ((kFReg || t < SI - 1) ? hv[t] : hg()[q]);
         sz += s[t] * z[t];
       }
     }
@@ -588,6 +645,39 @@ struct RegCtx {
     factor_chain<false>();
   }
 
+  // The two 4x4 foot blocks of Phi_u = H_u + beta + G^T Lambda G of per-stage task fl = 2 i + f
+  // (Lambda in VV), inverted; kept in this lane's registers (ph) and in dst[20 i + 10 f ..] for the
+  // S_ii build
+  __device__ void foot_inverse(int fl, double* dst) {
+    const double *VV = at(Lo::VV), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
+    const int i = fl >> 1, f = fl & 1;
+    double a[10];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? Hu[foot_colj(f, r)] + kBeta : 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // + G_k^T lam_k G_k over row k's structural nonzeros
+      const double lam = VV[16 * i + 8 * f + k];
+      const double* g4 = Gf + g_row(8 * f + k);
+      const double gz = g4[2];
+      a[5] += lam * gz * gz;  // (fz, fz)
+      if (k < 6) {
+        const int o = g_other(k);  // fx, fy or my (k is unrolled: constant)
+        const double go = g4[o];
+        a[o * (o + 1) / 2 + o] += lam * go * go;
+        if (o < 2) a[3 + o] += lam * gz * go;  // (fz, o)
+        else a[8] += lam * go * gz;            // (my, fz)
+      }
+    }
+    sweep_inverse<4>(a);  // IEEE pivots: Phi_f reaches cond ~1e7 as the barrier sharpens
+#pragma unroll
+    for (int e = 0; e < 10; ++e) {
+      if constexpr (!kPipe) ph[e] = a[e];
+      dst[20 * i + 10 * f + e] = a[e];
+    }
+  }
+
   // Phi_u foot inverses and the S_ii blocks (parallel over the wave)
   SRBD_PHASE_ATTR __device__ void factor_build() {
     const int lane = fresh_lane();
@@ -604,34 +694,7 @@ struct RegCtx {
       }
     }
     qp_sync<TPB>();
-    if (lane < 2 * N) {  // foot blocks of Phi_u, inverted; kept in this lane's registers
-      const int i = lane >> 1, f = lane & 1;
-      double a[10];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] = (r == c) ? Hu[foot_colj(f, r)] + kBeta : 0.0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // + G_k^T lam_k G_k over row k's structural nonzeros
-        const double lam = VV[16 * i + 8 * f + k];
-        const double* g4 = Gf + g_row(8 * f + k);
-        const double gz = g4[2];
-        a[5] += lam * gz * gz;  // (fz, fz)
-        if (k < 6) {
-          const int o = g_other(k);  // fx, fy or my (k is unrolled: constant)
-          const double go = g4[o];
-          a[o * (o + 1) / 2 + o] += lam * go * go;
-          if (o < 2) a[3 + o] += lam * gz * go;  // (fz, o)
-          else a[8] += lam * go * gz;            // (my, fz)
-        }
-      }
-      sweep_inverse<4>(a);  // IEEE pivots: Phi_f reaches cond ~1e7 as the barrier sharpens
-#pragma unroll
-      for (int e = 0; e < 10; ++e) {
-        ph[e] = a[e];
-        PHs[20 * i + 10 * f + e] = a[e];
-      }
-    }
+    if (lane < 2 * N) foot_inverse(lane, PHs);  // (FB = 0 here)
     qp_sync<TPB>();
     // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in two divergence-free passes over the class-sorted entry
     // table (TRI = c_tab.dvo: 21 dense x dense entries, then 57 with a sparse index): an entry
@@ -713,8 +776,10 @@ struct RegCtx {
 
   // kFwd: also the affine solve's forward elimination w_i = D_i^-1 (g_i - C w_{i-1}) with each
   // block's inverse row still in registers (g from solve_rhs(0) in QV; w_i written back over g_i)
-  template <bool kFwd>
-  SRBD_PHASE_ATTR __device__ void factor_chain() {
+  // kWait (stage-pipelined factorisation): step t first waits until wave 1 has published the stages
+  // it reads (pipe_need(t) of them, flag values tag + count)
+  template <bool kFwd, bool kWait = false>
+  SRBD_PHASE_ATTR __device__ void factor_chain(int tag = 0) {
     const int lane = fresh_lane();
     double* DV = at(Lo::DV);
     double* QV = at(Lo::QV);
@@ -754,6 +819,7 @@ struct RegCtx {
 #pragma unroll
         for (int c = 0; c < 12; ++c) X[c] = 0.0;
         const int imm = mstep ? kDvBytes * (N - 1) : 2 * kDvBytes * t;  // this step's blocks
+        if constexpr (kWait) pipe_wait(tag + pipe_need(t), t == 0);
         if (act) {
           if (!(mstep && g == 1)) {
 #pragma unroll
@@ -793,7 +859,7 @@ struct RegCtx {
           }
         }
         if (act && !(mstep && g == 1)) {
-          inverse_rows12(Sr, Dr);
+          inverse_rows12<kSwpInv>(Sr, Dr);
           // every lane writes its whole row: (r, c) and (c, r) share a packed slot, so each slot is
           // written twice with the two (rounding-different) halves of the symmetric inverse; the
           // later ds_write in program order wins, deterministically (shadow lanes 12..15 repeat row
@@ -812,6 +878,188 @@ struct RegCtx {
     }
     qp_sync<TPB>();
     PROF_ADD(2);
+  }
+
+  // ---------------------------------------------- stage-pipelined factorisation ----
+  // Two-wave QPs (kPipe): the block chain runs on wave 0 while wave 1 forms the stage blocks S_ii
+  // (DV), stage by stage in the order the chain consumes them, and publishes them through a flag word
+  // in LDS; the chain waits on it per step (s_sleep), not on a workgroup barrier. In the barrier-phased
+  // order (factor_build, solve_rhs<0>, factor_chain<true>) wave 1 idled through the whole chain
+  // (SQ_WAIT_ANY 55 % of an N = 20 wave's cycles, profiles/r04/sq_counters_fused_N20*). Same
+  // arithmetic in the same order per value (the sparse entries add their structural-zero slots as
+  // exact zeros). Built and measured 0.9-10 % SLOWER than the barrier-phased order (five variants,
+  // profiles/r05/n20_pipeline.txt): the chain waits for wave 1's per-iteration set-up and first stage
+  // pair, which is about what the barrier phase cost; off by default (SRBD_PIPE_FACTOR).
+  // k-th stage wave 1 produces: the pairs (t, N - 1 - t) of the steps both groups run, then group 0's
+  // remaining steps, the middle stage last
+  __device__ static int pipe_stage(int k) {
+    if (k == N - 1) return mid;
+    if (k < 2 * nb) return (k & 1) ? N - 1 - (k >> 1) : (k >> 1);
+    return nb + (k - 2 * nb);
+  }
+  // stages published before chain step t may start (the middle step, t = T: all of them)
+  __device__ static constexpr int pipe_need(int t) {
+    return t == T ? N : ((t + 1 < nf ? t + 1 : nf) + (t + 1 < nb ? t + 1 : nb));
+  }
+  __device__ int* pipe_flag() const { return reinterpret_cast<int*>(at(Lo::SG) + 14); }  // SG[14] unused
+  __device__ void pipe_wait(int want, bool first = false) {
+    const volatile int* f = pipe_flag();
+    const unsigned long long t0 = PROF_NOW();
+    (void)t0;
+    (void)first;
+    while (*f < want) __builtin_amdgcn_s_sleep(1);
+    PROF_SPAN(7, t0);  // diagnostic builds: cycles the chain waited for wave 1
+    if (first) PROF_SPAN(8, t0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  // factor_build + solve_rhs<0> + factor_chain<true> of a two-wave QP; tag: flag base of this
+  // iteration (64 it: a published count never reaches the next iteration's base)
+  SRBD_PHASE_ATTR __device__ void pipe_factor(int tag) {
+    const int lane = fresh_lane();
+    double *VV = at(Lo::VV), *DV = at(Lo::DV), *TV = at(Lo::TV), *QV = at(Lo::QV), *Zr2 = at(Lo::Z),
+           *PH = at(Lo::PH);
+    const double *IX = at(Lo::IX), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *K0 = at(Lo::K0),
+                 *K1 = at(Lo::K1);
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // W, D^-1, Lambda (factor_build's rows)
+      const int q = lane + TPB * t;
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
+        wd[t] = rcp3(s[t]) * z[t] + kDelta;
+        di[t] = rcp3(1.0 + kDelta * wd[t]);
+        VV[q] = di[t] * wd[t];
+      }
+    }
+    qp_sync<TPB>();
+    const int fl = lane - FB;
+    if ((unsigned)fl < 2u * N) foot_inverse(fl, PH);  // wave 1's lanes: the per-stage tasks live there
+    qp_sync<TPB>();
+#pragma unroll
+    for (int t = 0; t < SI; ++t) {  // solve_rhs<0>'s rows: r2 (parked in Z), VV = D^-1 (r2 + W r_s)
+      const int q = lane + TPB * t;
+      if (RegCtx<N>::full_slot(t, m) || q < m) {
+        const double si = rcp3(s[t]);
+        const double r2 = -(si * (s[t] * z[t]));
+        Zr2[q] = r2;
+        VV[q] = di[t] * (r2 + wd[t] * rs[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < SX; ++t) {  // the x columns of t
+      const int c = lane + TPB * t;
+      if (full_slot(t, nx) || c < nx) TV[c] = -rxx[t] * IX[c - m24(div12(c), 12)];
+    }
+    qp_sync<TPB>();
+    rhs_tasks<0>(fl, false);  // t on the foot and scalar u columns
+    qp_sync<TPB>();
+    g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
+    g_slot<1>(TV, Mc, Pd, Nd, QV);
+    qp_sync<TPB>();
+    if (__builtin_amdgcn_readfirstlane(lane) >= 64) {  // ---- wave 1: producer (wave-uniform branch) ----
+      const unsigned long long tsplit = PROF_NOW();
+      (void)tsplit;
+      const int lw = lane & 63;
+      double W[20], WB[8];
+      int slA, slB;
+      double kA0, kA1, kB0, kB1;
+      {
+        const int ix = pipe_ix;
+        const int ra = ix & 15, ca = (ix >> 4) & 15, rb = (ix >> 8) & 15, cb = (ix >> 12) & 15;
+        const int sya = ra * (ra + 1) / 2 + ca, syb = rb * (rb + 1) / 2 + cb;
+        slA = (ix >> 16) & 127;
+        slB = (ix >> 23) & 127;
+        kA0 = K0[sya];
+        kA1 = K1[sya];
+        if (ix >> 30) {  // dense x dense (factor_build's w)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            double vr[4], vc[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+              vr[a] = Nd[nd_idx(ra, foot_colj(f, a))];
+              vc[a] = Nd[nd_idx(ca, foot_colj(f, a))];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+              for (int b = 0; b <= a; ++b)
+                W[10 * f + a * (a + 1) / 2 + b] = a == b ? vr[a] * vc[a] : vr[a] * vc[b] + vr[b] * vc[a];
+          }
+        } else {  // sparse index (factor_build's wn at slots sym_idx(as, b))
+          const bool rsp = (ra % 6) >= 3;
+          const int sp = rsp ? ra : ca, dn = rsp ? ca : ra, as = sp % 3;
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const double ns = Nd[nd_idx(sp, foot_colj(f, as))];
+            double wn[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) wn[b] = ns * Nd[nd_idx(dn, foot_colj(f, b))];
+#pragma unroll
+            for (int e = 0; e < 10; ++e) {  // slot e = sym_idx(as, b) holds wn[b], the others 0
+              double v = 0.0;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) v = (sym_idx_c(as, b) == e) ? wn[b] : v;
+              W[10 * f + e] = v;
+            }
+          }
+        }
+        kB0 = K0[syb];
+        kB1 = K1[syb];
+        const bool rspb = (rb % 6) >= 3;
+        const int spb = rspb ? rb : cb, dnb = rspb ? cb : rb;  // foot position spb % 3 = 2
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const double ns = Nd[nd_idx(spb, foot_colj(f, 2))];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) WB[4 * f + b] = ns * Nd[nd_idx(dnb, foot_colj(f, b))];
+        }
+    
+      }
+      // Each lane of wave 1 holds the weights of S_ii entries for the whole pass: pass A, every lane,
+      // entry c_pipe_entry[lw] with its stage-invariant products expanded to the 20 packed Phi^-1 slots
+      // (a dense x dense entry: the 10 pair products per foot of factor_build; a sparse-index entry: its
+      // 4 products per foot at slots sym_idx(as, b), zeros elsewhere -- the nonzero terms then add in
+      // factor_build's order); pass B, lanes < 14, one more sparse entry of foot position as = 2 (the
+      // 21 dense + 57 sparse entries = 64 + 14; 14 of the 21 as = 2 entries go to pass B)
+      PROF_SPAN(10, tsplit);
+      // stage i's block: both passes from the stage's 20 Phi^-1 values (16-byte broadcast reads)
+      auto sii_stage = [&](int i) {
+        double P[20];
+        const double2* p2 = reinterpret_cast<const double2*>(PH + 20 * i);
+#pragma unroll
+        for (int e = 0; e < 10; ++e) {
+          const double2 v2 = p2[e];
+          P[2 * e] = v2.x;
+          P[2 * e + 1] = v2.y;
+        }
+        double va = i == 0 ? kA0 : kA1;
+#pragma unroll
+        for (int e = 0; e < 20; ++e) va += P[e] * W[e];
+        DV[kDvStride * dv_pos<N>(i) + slA] = va;
+        if (lw < 14) {
+          double vb = i == 0 ? kB0 : kB1;
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) vb += P[10 * f + sym_idx_c(2, b)] * WB[4 * f + b];
+          DV[kDvStride * dv_pos<N>(i) + slB] = vb;
+        }
+      };
+      // the chain's first step (stages 0 and N - 1) from both waves before it starts, one stage each
+#pragma unroll 1
+      for (int k = 0; k < N; ++k) {
+        sii_stage(pipe_stage(k));
+        if (k >= 2 * nb || (k & 1)) {  // publish the step's stages
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lw == 0) *(volatile int*)pipe_flag() = tag + k + 1;
+          if (k == 1) PROF_SPAN(9, tsplit);
+        }
+      }
+      PROF_ADD(2);  // diagnostic builds: wave 1's production time (slot 8 + 2)
+    } else {  // ---- wave 0: the chain, step by step as its stages are published ----
+      factor_chain<true, true>(tag);  // (ends in the workgroup barrier both waves meet below)
+      return;
+    }
+    qp_sync<TPB>();
   }
 
   // ------------------------------------------------------------------------ solve ----
@@ -890,8 +1138,9 @@ struct RegCtx {
       }
     }
     qp_sync<TPB>();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
-    if (lane < 2 * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
-      const int i = lane >> 1, f = lane & 1, b = 12 * i;
+    const int fl = lane - FB;
+    if ((unsigned)fl < 2u * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
+      const int i = fl >> 1, f = fl & 1, b = 12 * i;
       const double* zf = Zd + 16 * i + 8 * f;
       const double* RXu = DYs;
       const double* g = Gf + g_row(8 * f);  // (G^T dz)_a over column a's structural rows (as solve_rhs)
@@ -911,7 +1160,8 @@ struct RegCtx {
         }
         gt[2] = gz0 + gz1;
       }
-      double e1[4];
+      double e1[4], P[10];
+      load_ph(fl, P);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         const int j = foot_colj(f, a);
@@ -922,7 +1172,7 @@ struct RegCtx {
       for (int a = 0; a < 4; ++a) {
         double t = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * e1[q];
+        for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * e1[q];
         TV[nx + b + foot_colj(f, a)] += t;
       }
     }
@@ -966,11 +1216,26 @@ struct RegCtx {
       if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[c - m24(div12(c), 12)];
     }
     qp_sync<TPB>();
-    // t = Phi^-1 r1~, r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows)
-    if (lane < ((kMode == 0 || rx) ? 3 : 2) * N) {
-      if (lane < 2 * N) {
-        const int i = lane >> 1, f = lane & 1, b = 12 * i;
-        double rv[4];
+    rhs_tasks<kMode>(lane - FB, rx);
+    qp_sync<TPB>();
+    g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
+    g_slot<1>(TV, Mc, Pd, Nd, QV);
+    qp_sync<TPB>();
+    PROF_ADD(3);
+  }
+
+  // solve_rhs's per-stage tasks fl = lane - FB: t = Phi^-1 r1~ on the foot columns (fl < 2 N),
+  // r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows), and the scalar u
+  // columns of t (2 N <= fl < 3 N, affine solve or rx only)
+  template <int kMode>
+  __device__ void rhs_tasks(int fl, bool rx) {
+    double* TV = at(Lo::TV);
+    const double *VV = at(Lo::VV), *RXu = at(Lo::RXu), *REm = at(Lo::REm), *Gf = at(Lo::Gf), *SG = at(Lo::SG);
+    if ((unsigned)fl < (unsigned)(((kMode == 0 || rx) ? 3 : 2) * N)) {
+      if (fl < 2 * N) {
+        const int i = fl >> 1, f = fl & 1, b = 12 * i;
+        double rv[4], P[10];
+        load_ph(fl, P);
         {
           const double* vv = VV + 16 * i + 8 * f;
           const double* g = Gf + g_row(8 * f);  // (G^T vv)_a over column a's structural rows
@@ -995,11 +1260,11 @@ struct RegCtx {
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * rv[q];
+          for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * rv[q];
           TV[nx + b + foot_colj(f, a)] = t;
         }
       } else {
-        const int i = lane - 2 * N, b = 12 * i;
+        const int i = fl - 2 * N, b = 12 * i;
         const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
         TV[nx + b + 6] = (kDelta * -RXu[b + 6] + SG[6] * r4a) * SG[8];  // SG[8] = 1 / (phi6 delta + e6^2)
         TV[nx + b + 9] = (kDelta * -RXu[b + 9] + SG[7] * r4b) * SG[9];
@@ -1007,11 +1272,6 @@ struct RegCtx {
         TV[nx + b + 11] = -RXu[b + 11] * SG[3];
       }
     }
-    qp_sync<TPB>();
-    g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
-    g_slot<1>(TV, Mc, Pd, Nd, QV);
-    qp_sync<TPB>();
-    PROF_ADD(3);
   }
 
   // Twisted block solve (pdipm_srbd.hpp FastCtx::solve), w / v in registers. kBackOnly: the
@@ -1124,14 +1384,16 @@ struct RegCtx {
         TV[c] = TV[c] - aty * IX[j];
       }
     }
-    if (lane < (kAffine ? 2 : 3) * N) {
-      const bool foot = kAffine || lane < 2 * N;
-      const int i = foot ? (lane >> 1) : lane - 2 * N;
+    const int fl = lane - FB;
+    if ((unsigned)fl < (unsigned)((kAffine ? 2 : 3) * N)) {
+      const bool foot = kAffine || fl < 2 * N;
+      const int i = foot ? (fl >> 1) : fl - 2 * N;
       const int b = nx + 12 * i;
       const double* yi = QV + 12 * i;
       if (foot) {
-        const int f = lane & 1;
-        double av[4];
+        const int f = fl & 1;
+        double av[4], P[10];
+        load_ph(fl, P);
 #pragma unroll
         for (int a = 0; a < 3; ++a) av[a] = ncol(Nd, foot_colj(f, a), yi, a);
         av[3] = ncol<false>(Nd, foot_colj(f, 3), yi, 0);
@@ -1139,7 +1401,7 @@ struct RegCtx {
         for (int a = 0; a < 4; ++a) {
           double t = 0.0;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
+          for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * av[q];
           const int o = b + foot_colj(f, a);
           TV[o] = TV[o] - t;
         }
@@ -1393,9 +1655,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double* Hg = solver_in(args, 0) + (size_t)env * nz;
     const double* Gg = solver_in(args, 1) + (size_t)env * nG;
     const double* Ag = solver_in(args, 2) + (size_t)env * nA;
-    C.fg = solver_in(args, 3) + (size_t)env * nz;
-    C.hg = solver_in(args, 4) + (size_t)env * m;
-    C.bg = solver_in(args, 5) + (size_t)env * p;
+    C.env_ = env;
     // ---- compact load (stage 0/1 slices) ----
     for (int e = lane; e < 144; e += TPB) {
       const int r = e / 12, j = e % 12;
@@ -1463,6 +1723,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     SG[7] = e9;
     SG[8] = 1.0 / (p6 * kDelta + e6 * e6);
     SG[9] = 1.0 / (p9 * kDelta + e9 * e9);
+    *reinterpret_cast<int*>(SG + 14) = 0;  // RegCtx::pipe_flag: nothing published yet
   }
   qp_sync<TPB>();
   if (lane < 24) {  // compact M and C (C = M diag(P / phi_x)); group 1's block is pi C^T pi^T
@@ -1548,6 +1809,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   const double* QV = smem + Lo::QV;
   const double* DYm = smem + Lo::DYm;
   const double* RXu = smem + Lo::RXu;
+  if constexpr (RegCtx<N, kFused>::kPipe) C.pipe_prep();
   PROF_MARK_CTX(C);
   const int n_iter = kFused ? fa.n_iter : args.n_iter;
   for (int it = 0; it < n_iter; ++it) {
@@ -1594,9 +1856,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       res2 = sqrt(C.block_sum(c));
     }
     PROF_ADD_CTX(C, 0);
-    C.factor_build();
-    C.template solve_rhs<0>(0.0);
-    C.template factor_chain<true>();  // + the affine forward elimination
+    if constexpr (RegCtx<N, kFused>::kPipe) {
+      C.pipe_factor(64 * it);  // the same three phases, wave 1 feeding wave 0's chain stage by stage
+    } else {
+      C.factor_build();
+      C.template solve_rhs<0>(0.0);
+      C.template factor_chain<true>();  // + the affine forward elimination
+    }
     C.template solve_chain<true>();
     if (degen) {  // full affine finish (rho needs all of dx), then the 4-row refinement
       C.template solve_finish<false, false>();
@@ -1744,7 +2010,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #endif
 
 // at most 2 waves per SIMD (<= 256 registers): 2 one-wave QPs (N <= 10) per SIMD, or the waves of
-// two-wave (N <= 21) and three-wave (N <= 32) QPs
+// two-wave (N <= 21), three-wave (N <= 24) and four-wave (N <= 32) QPs
 template <int N>
 __global__ __launch_bounds__(reg_tpb(N), 2) SRBD_NO_DS_PAIRING void pdipm_srbd_reg_kernel(SolverArgs args) {
   reg_kernel_body<N, false>(args, FusedArgs{});

@@ -235,6 +235,8 @@ __host__ __device__ inline int a_pidx(const Tables& t, int N, int i, int r) {
 #define PROF_MARK()
 #define PROF_ADD(k)
 #define PROF_FLUSH(ctx)
+#define PROF_SPAN(k, t0)  // cycles since t0 into slot k (t0 from PROF_NOW)
+#define PROF_NOW() 0ull
 #endif
 
 // 1/d: v_rcp_f64 (~2^-24 relative) refined by one Newton step y (1 + e), e = 1 - d y: relative

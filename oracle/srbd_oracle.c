@@ -470,6 +470,8 @@ typedef struct {
 /* ldl_numeric (up-looking LDL^T, no pivoting) */
 static int ldl_numeric(const pattern_t *P, ldl_work *w) {
   const int n = P->n;
+  int fail = 0;  /* first zero pivot (1-based); the factorisation still runs to the end, so every column
+                    of L has its pattern and ldl_solve stays in bounds (the values are then inf / NaN) */
   for (int k = 0; k < n; ++k) {
     w->Y[k] = 0.0;
     int top = n;
@@ -503,9 +505,9 @@ static int ldl_numeric(const pattern_t *P, ldl_work *w) {
       w->Lx[q] = l_ki;
       w->Lnz[i]++;
     }
-    if (w->D[k] == 0.0) return k + 1;
+    if (w->D[k] == 0.0 && !fail) fail = k + 1;
   }
-  return 0;
+  return fail;
 }
 
 /* ldl_solve: x = P^T L^-T D^-1 L^-1 P b  (b overwritten with the solution) */

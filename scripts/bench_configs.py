@@ -26,7 +26,7 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "configs.json")
     rows = []
     for name, args in CONFIGS:
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5", "--no-dropin", *args]
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5", "--no-dropin", "--no-config3", *args]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
         if r.returncode != 0:
             raise SystemExit(f"{name}: bench.py failed\n{r.stdout}\n{r.stderr}")

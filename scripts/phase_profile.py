@@ -11,10 +11,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-LIB = "/tmp/libsrbd_mpc_prof.so"
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), "-o", LIB, os.path.join(ROOT, "biped_pympc_amd/csrc/srbd_mpc.hip")],
-               check=True)
+LIB = os.environ.get("PHASE_LIB")  # prebuilt instrumented library (N = 20: scripts/build_variant.py
+#   OUT --no-regn --reg20=-include --reg20=scripts/phase_prof.hpp, stamps in the N = 20 unit only)
+if not LIB:
+    LIB = "/tmp/libsrbd_mpc_prof.so"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-include", os.path.join(ROOT, "scripts", "phase_prof.hpp"), "-o", LIB,
+                    os.path.join(ROOT, "biped_pympc_amd/csrc/srbd_mpc.hip")], check=True)
 os.environ["SRBD_LIB"] = LIB
 
 import numpy as np  # noqa: E402
@@ -33,7 +36,7 @@ inputs = [torch.from_numpy(a).cuda() for a in wl.inputs]
 bufs = solver.MPCSolveBuffers.allocate(N, B)
 solver.mpc_solve(inputs, N, K, buffers=bufs)
 torch.cuda.synchronize()
-acc = (ctypes.c_ulonglong * 16)()
+acc = (ctypes.c_ulonglong * 32)()
 L.srbd_debug_phase_cycles(acc)  # reset
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
@@ -45,7 +48,18 @@ names = ["residuals", "factor: parallel (W, Phi_u blocks, S_ii)", "factor: stage
          "solve: parallel parts (x3)", "solve: fwd/bwd chains (x3)", "step lengths / update",
          "refinement residuals (KKT rows 1, 4)"]
 tot = sum(acc[k] for k in range(7))
-print(f"N={N} B={B} K={K}: step {e0.elapsed_time(e1):.3f} ms; cycles per QP per iteration:")
+print(f"N={N} B={B} K={K}: step {e0.elapsed_time(e1):.3f} ms; cycles per QP per iteration (wave 0):")
 for k, n in enumerate(names):
     print(f"  {n:45s} {acc[k] / B / K:10.0f}  ({100 * acc[k] / tot:5.1f} %)")
 print(f"  {'total':45s} {tot / B / K:10.0f}")
+extra = {7: "the chain waited for wave 1 (all steps)", 8: "  of which before step 0",
+         9: "wave 1: split -> first stage pair published", 10: "wave 1: producer weights set up"}
+for k, n in extra.items():
+    if acc[k] or acc[16 + k]:
+        print(f"  {n:45s} {acc[k] / B / K:10.0f} (wave 0) {acc[16 + k] / B / K:10.0f} (wave 1)")
+if any(acc[16 + k] for k in range(7)):  # wave 1 of a two-wave QP (its own phase boundaries)
+    tot1 = sum(acc[16 + k] for k in range(7))
+    print("wave 1:")
+    for k, n in enumerate(names):
+        print(f"  {n:45s} {acc[16 + k] / B / K:10.0f}  ({100 * acc[16 + k] / tot1:5.1f} %)")
+    print(f"  {'total':45s} {tot1 / B / K:10.0f}")
