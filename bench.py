@@ -68,6 +68,8 @@ def parse(argv=None):
     p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
     p.add_argument("--no-dropin", action="store_true",
                    help="skip the reference caller's CusADi schedule leg (1 former + 4 x 5-iteration evaluate)")
+    p.add_argument("--sustain-seconds", type=float, default=3.0,
+                   help="after the timed steps, run the step kernel back to back for this long (0: skip)")
     p.add_argument("--no-config3", action="store_true",
                    help="skip the BASELINE config-3 leg (fused N = 20, B = 4096, K = 10 kernel + oracle sample)")
     p.add_argument("--dump-u0", default=None,
@@ -386,6 +388,21 @@ def dropin_leg(inputs, N: int, B: int, reps: int) -> dict:
 C3_N, C3_B, C3_K, C3_SAMPLE = 20, 4096, 10, 64
 
 
+def sustained_leg(fn, B: int, seconds: float, burst: int = 250) -> dict:
+    """The step kernel back to back for `seconds` in bursts of `burst` launches, each burst timed with
+    HIP events on the launch stream: the steady-state rate (clocks and power settled, no idle gaps) and
+    the spread over bursts. Also gives the driver's GPU-activity sampler a window of real load."""
+    per = []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        per.append(event_time_ms(fn, burst, warm=0))
+    per = np.array(per)
+    return {"seconds": round(time.perf_counter() - t0, 2), "launches": int(len(per) * burst),
+            "solves_per_s": round(B / (per.mean() * 1e-3), 1), "ms_per_launch_mean": round(float(per.mean()), 4),
+            "ms_per_launch_min_burst": round(float(per.min()), 4), "ms_per_launch_max_burst": round(float(per.max()), 4),
+            "burst": burst}
+
+
 def config3_leg(dev, reps: int) -> dict:
     """BASELINE config 3 (batch 4096, horizon N = 20, 10 iterations, one GPU): the fused step kernel
     (mpc_step_reg_kernel<20>: former + cold PDIPM, one launch) timed with HIP events on the launch
@@ -517,6 +534,9 @@ def main(argv=None):
         ms_gather = event_time_ms(lambda: sh.gather_u0(u0), a.kernel_reps)
     ranks = rank_spread(dist, dev if backend == "nccl" else torch.device("cpu"), ms_fused,
                         ms_gather or 0.0, own_elapsed)
+    sustained = None
+    if a.sustain_seconds > 0:
+        sustained = sustained_leg(lambda: solver.mpc_solve(inputs, N, K, 1.0, buffers=bufs), B, a.sustain_seconds)
     # BASELINE config 3 (batch 4096, N = 20, K = 10) under the driver's clock: its fused step kernel
     # timed with HIP events (+ a 64-env oracle parity sample in the CPU leg below)
     c3 = None
@@ -684,6 +704,7 @@ def main(argv=None):
             # the reference caller's own schedule through the CusADi-ABI drop-ins (INTEGRATION.md option A)
             "dropin_step_ms": None if dropin is None else dropin["literal_ms"],
             "dropin_step": dropin,
+            "sustained": sustained,  # this rank's step kernel back to back for --sustain-seconds
             "config3": c3,  # BASELINE configs[2]: batch 4096, N = 20, 10 iterations, one GPU
             "ranks": ranks,  # N > 1: per-rank solve / gather / timed-region spread
         }

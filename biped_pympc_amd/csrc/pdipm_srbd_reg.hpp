@@ -438,10 +438,15 @@ struct RegCtx {
   static constexpr int kFactorUnroll = T + 1;  // chains fully unrolled (N = 20: -4.7 % vs rolled)
   double* L;
   int lane;
-  // The CCS kernel's f, h, b rows of this env, addressed from the kernel's own argument (kernarg
-  // segment: scalar loads) at each use: a 64-bit row pointer held across the Newton loop is what the
-  // N = 21 kernel spilled (a scratch reload per iteration). Unused by the fused kernel (kFReg).
+  // The CCS kernel's f, h, b rows of this env. At N = 21 they are addressed from the kernel's own
+  // argument (kernarg segment: scalar loads) at each use: a 64-bit row pointer held across the Newton
+  // loop is what that kernel spilled (a scratch reload per iteration). Elsewhere the three row
+  // pointers are held (the per-use address arithmetic cost the N = 10 kernel ~1 %,
+  // profiles/r05/ab_*.txt). tests/test_isa_hazards.py checks the choice at every horizon. Unused by the
+  // fused kernel (kFReg).
+  static constexpr bool kArgRows = N == 21;
   int env_ = 0;
+  const double *fp_ = nullptr, *hp_ = nullptr, *bp_ = nullptr;
   // the pipelined S_ii build's two entries of this lane (pipe_factor), looked up once per solve:
   // rows / columns of the pass-A and pass-B entries and their DV slots, 4 + 4 + 4 + 4 + 7 + 7 bits
   int pipe_ix = 0;
@@ -453,9 +458,9 @@ struct RegCtx {
     const int sla = c_dvslot[ra * (ra + 1) / 2 + ca], slb = c_dvslot[rb * (rb + 1) / 2 + cb];
     pipe_ix = ra | (ca << 4) | (rb << 8) | (cb << 12) | (sla << 16) | (slb << 23) | ((ka < 21) << 30);
   }
-  __device__ const double* fg() const { return solver_in(kernel_args(), 3) + (size_t)env_ * nz; }
-  __device__ const double* hg() const { return solver_in(kernel_args(), 4) + (size_t)env_ * m; }
-  __device__ const double* bg() const { return solver_in(kernel_args(), 5) + (size_t)env_ * p; }
+  __device__ const double* fg() const { return kArgRows ? solver_in(kernel_args(), 3) + (size_t)env_ * nz : fp_; }
+  __device__ const double* hg() const { return kArgRows ? solver_in(kernel_args(), 4) + (size_t)env_ * m : hp_; }
+  __device__ const double* bg() const { return kArgRows ? solver_in(kernel_args(), 5) + (size_t)env_ * p : bp_; }
   // this lane's entries of f (x and u columns), b and h, held in registers for the whole solve:
   // set once (loaded, or as the fused kernel computes them), never re-read from memory
   double fxr[SX], fur[SX], bvr[SE], hvr[SI];
@@ -1656,6 +1661,11 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double* Gg = solver_in(args, 1) + (size_t)env * nG;
     const double* Ag = solver_in(args, 2) + (size_t)env * nA;
     C.env_ = env;
+    if constexpr (!RegCtx<N, kFused>::kArgRows) {
+      C.fp_ = solver_in(args, 3) + (size_t)env * nz;
+      C.hp_ = solver_in(args, 4) + (size_t)env * m;
+      C.bp_ = solver_in(args, 5) + (size_t)env * p;
+    }
     // ---- compact load (stage 0/1 slices) ----
     for (int e = lane; e < 144; e += TPB) {
       const int r = e / 12, j = e % 12;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 evidence in one GPU call (after scripts/gpu_r04.sh passed): smoke, the default bench line,
+# Round-5 evidence in one GPU call (after scripts/gpu_r05.sh passed): smoke, the default bench line,
 # the driver-form run, rocprofv3 kernel stats of the bench command, PMC traffic (FETCH_SIZE, WRITE_SIZE)
 # and SQ utilisation passes, the per-config rates, and a two-rank rehearsal of the rank launcher on one
 # device over gloo. Output: gpurun_out/r05p/ (summarised into profiles/r05/ on the build host).
@@ -8,12 +8,12 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/r05p
 mkdir -p $O
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --no-config3 --kernel-reps 2"
-B20="python3 bench.py --horizon 20 --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --no-config3 --kernel-reps 2"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --no-config3 --sustain-seconds 0 --kernel-reps 2"
+B20="python3 bench.py --horizon 20 --steps 3 --warmup 1 --no-cpu-baseline --no-controller --no-dropin --no-config3 --sustain-seconds 0 --kernel-reps 2"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && \
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $O/bench_driver_form.json 2> $O/bench_driver_form.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_stats -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-controller --no-dropin --no-config3 > $O/bench_prof.json 2> $O/prof.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_stats -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-controller --no-dropin --no-config3 --sustain-seconds 0 > $O/bench_prof.json 2> $O/prof.err && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B > $O/pmc1.json 2> $O/pmc1.err && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B > $O/pmc2.json 2> $O/pmc2.err && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES -d $O/pmc_sq -o run --output-format csv -- $B > $O/pmc_sq.json 2> $O/pmc_sq.err && \

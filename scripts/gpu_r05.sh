@@ -16,8 +16,8 @@ if [ -z "$SKIP_BENCH" ]; then
   tail -c 3000 $O/bench.json
 fi
 if [ -n "$AB" ]; then
-  { echo "# N=10 (fused_ms pdipm_ms value max_rel_du)"; AB_OLD=ab/libsrbd_mpc_r04.so bash scripts/ab_bench.sh ${AB_ROUNDS:-2} &&
-    echo "# N=20" && AB_OLD=ab/libsrbd_mpc_r04.so bash scripts/ab_bench.sh ${AB_ROUNDS:-2} --horizon 20 --no-controller; } 2>&1 | grep -v amdgpu.ids > $O/ab.txt
+  { echo "# N=10 (fused_ms pdipm_ms value max_rel_du)"; AB_OLD=${AB_LIB:-ab/libsrbd_mpc_r04.so} bash scripts/ab_bench.sh ${AB_ROUNDS:-2} --sustain-seconds 0 --no-config3 &&
+    echo "# N=20" && AB_OLD=${AB_LIB:-ab/libsrbd_mpc_r04.so} bash scripts/ab_bench.sh ${AB_ROUNDS:-2} --sustain-seconds 0 --horizon 20 --no-controller; } 2>&1 | grep -v amdgpu.ids > $O/ab.txt
   cat $O/ab.txt
 fi
 exit 0

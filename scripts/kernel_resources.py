@@ -1,6 +1,9 @@
 """Per-kernel register / spill / scratch figures from a hipcc -S listing (the AMDGPU metadata).
 
     python scripts/kernel_resources.py /tmp/main.s [substring]
+    python scripts/kernel_resources.py --table > profiles/rNN/kernel_resources.txt
+        (compiles every product unit to device ISA with the product flags, srbd_regN.hip in its six
+        horizon parts, and prints one row per kernel)
 """
 import re
 import sys
@@ -42,6 +45,47 @@ def body_spills(path, kernel, window=12):
     return out
 
 
+def table(tmpdir="/tmp/kernel_resources"):
+    """The kernel_resources.txt table of every product translation unit (product flags)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from biped_pympc_amd.build import HIP_UNITS, source_hash, unit_compile_cmd
+    os.makedirs(tmpdir, exist_ok=True)
+    jobs = []
+    for unit in HIP_UNITS:
+        parts = [[f"-DSRBD_REGN_PART={k}"] for k in range(6)] if unit == "srbd_regN.hip" else [[]]
+        for k, defs in enumerate(parts):
+            out = os.path.join(tmpdir, f"{unit}.{k}.s")
+            tag = f"{unit}/{k}" if len(parts) > 1 else unit
+            cmd = unit_compile_cmd(unit, [*defs, "--cuda-device-only", "-S", "-o", out])
+            jobs.append((tag, out, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)))
+    rows = []
+    for tag, out, p in jobs:
+        err = p.communicate()[1]
+        if p.returncode:
+            raise SystemExit(err.decode()[-2000:])
+        for name, r in resources(out).items():
+            dem = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+            dem = re.sub(r"\(.*\)$", "", dem)
+            rows.append((tag, dem, r))
+    print(f"# Per-kernel resources from the gfx950 device ISA (hipcc --cuda-device-only -S, product flags;\n"
+          f"# scripts/kernel_resources.py --table). Sources at build id {source_hash()}. vgpr = arch VGPRs, spill =\n"
+          f"# VGPR spills as the compiler reports them (the CCS kernels' one or two: the whole-wave save around the\n"
+          f"# fallback call, see tests/test_isa_hazards.py), scratch = private segment bytes per lane (call stack),\n"
+          f"# lds = static LDS.")
+    print(f"{'unit':18s} {'kernel':52s} {'vgpr':>4s} {'agpr':>4s} {'spill':>5s} {'sgpr_spill':>10s} {'scratch':>7s} {'lds':>5s}")
+    fmt = lambda v: "-" if v is None else str(v)
+    for tag, dem, r in rows:
+        print(f"{tag:18s} {dem[:52]:52s} {fmt(r['vgpr_count']):>4s} {fmt(r['agpr_count']):>4s} "
+              f"{fmt(r['vgpr_spill_count']):>5s} {fmt(r['sgpr_spill_count']):>10s} "
+              f"{fmt(r['private_segment_fixed_size']):>7s} {fmt(r['group_segment_fixed_size']):>5s}")
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["--table"]:
+        table()
+        sys.exit(0)
     for n, r in resources(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "").items():
         print(f"{n[:60]:60s} " + " ".join(f"{k}={v}" for k, v in r.items()))
