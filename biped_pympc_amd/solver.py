@@ -6,7 +6,6 @@ Tensors are batched row-major ``(B, nnz)`` FP64 on the GPU, exactly the CusADi l
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 
 import torch
 
@@ -119,19 +118,34 @@ def pdipm_ccs(qp: list[torch.Tensor], x_init: torch.Tensor, N: int, n_iter: int,
     return outputs
 
 
-@dataclass
 class MPCSolveBuffers:
-    """Preallocated device buffers for repeated ``mpc_solve`` calls (no allocation per step)."""
-    N: int
-    B: int
-    workspace: torch.Tensor
-    outputs: list
+    """Preallocated device buffers for repeated ``mpc_solve`` calls (no allocation per step).
+
+    ``outputs`` are allocated up front; the QP ``workspace`` (H, f, A, b, G, d: 18 KB per env at
+    N = 10) only on first use -- the two-kernel form, ``keep_qp`` or ``qp_views`` -- since the fused
+    step never writes it (at 8192 envs it is 148 MB of HBM the default path would hold for nothing)."""
+
+    def __init__(self, N: int, B: int, device, outputs: list, workspace: torch.Tensor | None = None):
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.N, self.B, self.device, self.outputs = N, B, dev, outputs
+        self._workspace = workspace
 
     @classmethod
     def allocate(cls, N: int, B: int, device="cuda") -> "MPCSolveBuffers":
-        n = _native.lib().srbd_mpc_workspace_doubles(N, B)
-        return cls(N, B, torch.empty(max(n, 1), dtype=torch.float64, device=device),
-                   _alloc_solver_outputs(B, N, device))
+        return cls(N, B, device, _alloc_solver_outputs(B, N, device))
+
+    @property
+    def workspace_allocated(self) -> bool:
+        return self._workspace is not None
+
+    @property
+    def workspace(self) -> torch.Tensor:
+        if self._workspace is None:
+            n = _native.lib().srbd_mpc_workspace_doubles(self.N, self.B)
+            self._workspace = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+        return self._workspace
 
     def qp_views(self) -> list[torch.Tensor]:
         """[H, f, A, b, G, d] views into the workspace (filled by the former)."""
@@ -163,8 +177,8 @@ def mpc_solve(former_inputs: list[torch.Tensor], N: int, n_iter: int, y0: float 
     if buffers is None or buffers.B != B or buffers.N != N:
         buffers = MPCSolveBuffers.allocate(N, B, former_inputs[0].device)
     _check_batch(buffers.outputs, d.solver_out_nnz, B, "mpc_solve outputs")
-    if buffers.workspace.device != former_inputs[0].device:
-        raise ValueError(f"mpc_solve: workspace on {buffers.workspace.device}, inputs on {former_inputs[0].device}")
+    if buffers.device != former_inputs[0].device:
+        raise ValueError(f"mpc_solve: buffers on {buffers.device}, inputs on {former_inputs[0].device}")
     L = _native.lib()
     # the fused kernel runs under the auto solver path (any horizon); otherwise the former writes the
     # whole QP into the workspace for the solver kernel

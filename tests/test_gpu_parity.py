@@ -491,6 +491,43 @@ def test_full_size_properties(N, B, random_gait):
     assert rel_err_rows(x[idx], ref[0]).max() <= dict(SOLVER_CASES)[K]
 
 
+@pytest.mark.parametrize("fused,reps", [(True, 2197), (False, 440)])
+def test_batches_past_32_bit_element_offsets(fused, reps):
+    """Maximum sizes: a batch whose arrays hold more than 2^31 elements, so every env row past that
+    point is reached only through 64-bit offsets (the kernels form them as (size_t)env * width). The
+    fused step at 2197 x 4096 = 8,998,912 envs (x: 240 per env, 2.16e9 elements, 51 GB of solution);
+    former + CCS solver at 440 x 4096 = 1,802,240 envs (A: 1196 per env, 2.16e9 elements in the
+    workspace). A 4096-env workload is tiled on the device and every env of the big batch must
+    reproduce its 4096-env solve bit for bit (a QP's solution does not depend on its batch position),
+    the 4096-env solve matches the oracle on a strided sample. Sized for one MI355X (288 GB HBM):
+    ~66 GB (fused) / ~52 GB (CCS)."""
+    N, K, B0 = 10, 10, 4096
+    d = layout.Dims(N)
+    width = d.nz if fused else d.nnz_A
+    assert reps * B0 * width > 2**31  # the test's premise
+    free, _ = torch.cuda.mem_get_info()
+    need = reps * B0 * 8 * (sum(d.former_in_nnz) + sum(d.solver_out_nnz)
+                            + (0 if fused else sum(d.former_out_nnz)))
+    if need > 0.8 * free:
+        pytest.skip(f"needs {need / 2**30:.0f} GiB of device memory, {free / 2**30:.0f} GiB free")
+    wl = make_workload(B0, N, seed=9100 + int(fused), random_gait=True, residuals=True)
+    small_in = _cuda(wl.inputs)
+    small = [t.clone() for t in solver.mpc_solve(small_in, N, K, y0=1.0, fused=fused)]
+    idx = np.arange(0, B0, B0 // 16)
+    ref = oracle.mpc_solve(N, K, [np.ascontiguousarray(a[idx]) for a in wl.inputs], y0=1.0)
+    assert rel_err_rows(small[0][idx].cpu().numpy(), ref[0]).max() <= dict(SOLVER_CASES)[K]
+    big_in = [t.repeat(reps, 1) for t in small_in]
+    del small_in
+    big = solver.mpc_solve(big_in, N, K, y0=1.0, fused=fused)
+    torch.cuda.synchronize()
+    del big_in
+    for b, s_ in zip(big, small):
+        assert b.shape[0] == reps * B0
+        assert bool((b.view(reps, B0, -1) == s_.view(1, B0, -1)).all()), "env rows differ from the 4096-env solve"
+    del big
+    torch.cuda.empty_cache()
+
+
 def test_empty_batch_is_a_no_op():
     N = 10
     wl = make_workload(1, N, seed=1)
@@ -558,11 +595,15 @@ def test_ccs_entry_from_arbitrary_x_init(N, K, tol):
 @pytest.mark.parametrize("N", [10, 20])
 def test_fused_step_qp_vectors_only_on_request(N):
     """srbd_mpc_solve_fused keeps f, b, d on chip by default; keep_qp writes them, equal to the
-    former's own rows, and the solution is the same either way."""
+    former's own rows, and the solution is the same either way. The QP workspace the default path
+    never writes is not allocated by it either (MPCSolveBuffers allocates it on first use)."""
     B = 37
     wl = make_workload(B, N, seed=800 + N, random_gait=True)
     ins = _cuda(wl.inputs)
     qp = solver.qp_former(ins, N)
+    lean = solver.MPCSolveBuffers.allocate(N, B, "cuda")
+    first = [t.clone() for t in solver.mpc_solve(ins, N, 10, buffers=lean)]
+    assert not lean.workspace_allocated
     bufs = solver.MPCSolveBuffers.allocate(N, B, "cuda")
     bufs.workspace.fill_(3.0)
     a = [t.clone() for t in solver.mpc_solve(ins, N, 10, buffers=bufs)]
@@ -570,8 +611,8 @@ def test_fused_step_qp_vectors_only_on_request(N):
     assert bool((bufs.workspace == 3.0).all())
     c = solver.mpc_solve(ins, N, 10, buffers=bufs, keep_qp=True)
     torch.cuda.synchronize()
-    for x, y in zip(a, c):
-        assert torch.equal(x, y)
+    for x, y, z in zip(a, c, first):
+        assert torch.equal(x, y) and torch.equal(x, z)
     views = bufs.qp_views()
     for k in (1, 3, 5):  # f, b, d
         assert torch.equal(views[k], qp[k]), k
