@@ -68,7 +68,7 @@ def parse(argv=None):
     p.add_argument("--no-controller", action="store_true", help="skip the controller-step timing (PMC passes)")
     p.add_argument("--no-dropin", action="store_true",
                    help="skip the reference caller's CusADi schedule leg (1 former + 4 x 5-iteration evaluate)")
-    p.add_argument("--sustain-seconds", type=float, default=3.0,
+    p.add_argument("--sustain-seconds", type=float, default=8.0,
                    help="after the timed steps, run the step kernel back to back for this long (0: skip)")
     p.add_argument("--no-config3", action="store_true",
                    help="skip the BASELINE config-3 leg (fused N = 20, B = 4096, K = 10 kernel + oracle sample)")
