@@ -49,6 +49,7 @@ struct SolverArgs {
   int scratch_slots;
   int scratch_stride;  // doubles per slot: the largest SolverLayout(N).total over N = 1..kMaxN
   int* status;  // (batch) per-problem status word (kStatus* bits), or null: not written
+  int refine_all;  // 1: the register kernels refine the affine direction in every iteration (srbd_set_refinement)
 };
 
 // Per-problem status word (SURVEY.md 5 "failure detection"; the reference has only its clamps,

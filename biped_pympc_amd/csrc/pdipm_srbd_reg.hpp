@@ -29,6 +29,12 @@
 #ifndef SRBD_SWP_INV
 #define SRBD_SWP_INV 0  // two-wave QPs invert their chain blocks by the software-pipelined sweep: measured slower, off
 #endif
+#ifndef SRBD_REFINE_AFFINE_ALL
+#define SRBD_REFINE_AFFINE_ALL 0  // refine the affine direction in every iteration (+18 % time; diagnostics)
+#endif
+#ifndef SRBD_AFFINE_REFINE_W
+#define SRBD_AFFINE_REFINE_W 1e3  // refine the affine direction when some row has z / s at least this
+#endif
 #ifndef SRBD_PIPE_FACTOR
 #define SRBD_PIPE_FACTOR 0  // stage-pipelined factorisation of two-wave QPs: built and measured slower, off
 #endif
@@ -1517,6 +1523,7 @@ struct FusedArgs {
   float* tau;      // (B, 2, ndof) float32, or null
   int ndof;
   int* status;     // (B) per-problem status word (pdipm.hpp kStatus*), or null
+  int refine_all;  // 1: refine the affine direction in every iteration (srbd_set_refinement)
 };
 
 // Body shared by the solver kernel (kFused = false: the QP comes from qp_former's CCS outputs and is
@@ -1836,18 +1843,23 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
-    // A degenerate iterate -- some s at its 1e-8 clamp (sparse_pdipm_solver.py:520) -- has rows
-    // with W = z / s up to ~1e8, where the reduced solve's affine ds, dz lose most digits; its error
-    // then enters sigma and the corrector (profiles/r02/refinement_4row.txt). Such iterations also
-    // refine the affine direction (the QP is one wave or two joined ones: a uniform branch).
+    // An ill-conditioned iterate -- some row with W = z / s >= SRBD_AFFINE_REFINE_W (1e3), e.g. an s
+    // at or near its 1e-8 clamp (sparse_pdipm_solver.py:520) -- is where the reduced solve's affine
+    // ds, dz lose digits; their error enters sigma and the corrector, and the trajectory drifts from the
+    // reference's (profiles/r02/refinement_4row.txt; round 5: scripts/parity_fuzz.py found iterates at
+    // W 4.5e3 .. 1.2e8 with s above the clamp drifting to 1e-4 in z, profiles/r05/parity_fuzz.txt).
+    // Such iterations also refine the affine direction (the QP is one wave or joined ones: a uniform
+    // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations. srbd_set_refinement(1)
+    // refines it in every iteration, as the LDS-resident and general kernels always do.
     bool degen;
     {
       const int l = C.fresh_lane();
       bool p = false;
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m) p = p || (C.s[t] <= 1e-8);
-      degen = C.block_any(p);
+        if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m)
+          p = p || (C.s[t] <= 1e-8) || (C.z[t] >= SRBD_AFFINE_REFINE_W * C.s[t]);
+      degen = SRBD_REFINE_AFFINE_ALL || (kFused ? fa.refine_all : args.refine_all) || C.block_any(p);
     }
     int ul = C.fresh_lane();
     if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)

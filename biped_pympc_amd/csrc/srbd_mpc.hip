@@ -75,6 +75,15 @@ int solver_path() {
   return p ? *p : 0;
 }
 
+// Affine refinement per device (srbd_set_refinement): 0 = on ill-conditioned iterates (z / s >= 1e3 in
+// some row, or an s at its clamp), 1 = in every iteration. Read by the register kernels only (the
+// LDS-resident and general kernels refine the affine direction in every iteration).
+srbd::PerDevice<int> g_refinement;
+int refinement_mode() {
+  const int* p = g_refinement.at(current_device());
+  return p ? *p : 0;
+}
+
 int ensure_lds_attr(const void* fn, size_t bytes, srbd::LdsAttr& cache) {
   const int dev = current_device();
   if (dev < 0) return set_error((int)hipErrorInvalidDevice, "no current HIP device (or index >= 64)");
@@ -202,6 +211,7 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
   static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20;
   srbd::SolverArgs a = a0;
+  a.refine_all = refinement_mode();
   const int path = solver_path();
   // the stage-invariant kernels solve any other QP of the batch in the same launch (scratch pool)
   if (path != 1)
@@ -304,6 +314,17 @@ int srbd_set_solver_path(int path) {
 }
 
 int srbd_get_solver_path(void) { return solver_path(); }
+
+int srbd_set_refinement(int mode) {
+  if (mode < 0 || mode > 1)
+    return set_error(kErrInvalid, "srbd_set_refinement: 0 (ill-conditioned iterates) or 1 (every iteration)");
+  int* p = g_refinement.at(current_device());
+  if (!p) return set_error((int)hipErrorInvalidDevice, "srbd_set_refinement: no current HIP device");
+  *p = mode;
+  return 0;
+}
+
+int srbd_get_refinement(void) { return refinement_mode(); }
 
 int srbd_prepare_device(void) {
   int rc = 0;
@@ -477,8 +498,10 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 // launch of the fused / controller-step kernel (a fully set up FusedArgs): the register kernels at
 // the horizons they are instantiated for (10, 20 and regN.hpp's), the LDS-resident one-launch step
 // (mpc_step_lds.hpp) at every other horizon
-static int launch_step(const srbd::FusedArgs& a, hipStream_t st) {
+static int launch_step(const srbd::FusedArgs& a0, hipStream_t st) {
   static srbd::LdsAttr cfg_lds;
+  srbd::FusedArgs a = a0;
+  a.refine_all = refinement_mode();
   if (srbd::regn::supported(a.N)) {
     srbd::regn::launch_step(a.N, a, st);  // static LDS (RegLayout)
   } else if (a.N != 10 && a.N != 20) {

@@ -134,6 +134,18 @@ int srbd_set_solver_path(int path);
  * register-resident kernel at N = 2..32, the LDS-resident step kernel at N = 1. */
 int srbd_get_solver_path(void);
 
+/* Affine-direction refinement of the register-resident kernels (the default solvers at N = 2..32), per
+ * device like the solver path. Every Newton iteration refines the combined direction once against the
+ * full KKT; the affine (predictor) direction, whose ds / dz set sigma and the corrector, is refined
+ * 0 = (default) in iterations with an ill-conditioned iterate: some row with z / s >= 1e3 or an s at its
+ * 1e-8 clamp -- where an unrefined predictor lets the trajectory drift from the reference's;
+ * 1 = in every iteration (as the LDS-resident and general kernels always do): the results then sit at
+ * the FP64 floor of the reference's own elimination in every configuration scripts/parity_fuzz.py
+ * draws, for ~18 % more time at N = 10. Returns 0, or an error for another mode. */
+int srbd_set_refinement(int mode);
+/* The refinement mode in effect for the current HIP device (0 if never set). */
+int srbd_get_refinement(void);
+
 /* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the
  * stage-invariant kernels (one slot per resident workgroup -- 2048 on an MI355X of
  * srbd_scratch_slot_bytes() = 162,000 B each: 332 MB of HBM per process and device, lock words

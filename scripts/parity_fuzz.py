@@ -1,0 +1,173 @@
+"""Randomised parity campaign on the GPU box: HIP path vs the oracle over random configurations.
+
+    python scripts/parity_fuzz.py [SECONDS] [OUT_JSON]     (default 150 s, gpurun_out/parity_fuzz.json)
+    FUZZ_CASES=n: exactly the first n cases of the fixed random sequence instead of a time budget
+    SRBD_LIB=path: another build of libsrbd_mpc.so (A/B of two libraries on the same cases)
+    FUZZ_REFINE=every_iteration: the register kernels' strict refinement mode (srbd_set_refinement(1))
+
+Each case draws a horizon N in 1..32, an iteration count K in 1..25, a batch B in 1..300, an entry
+(fused step with y0 in {0, 1}; the solver from the GPU caller's cold init; the solver warm-started
+from the oracle's iterate after K0 iterations -- the reference caller's chained calls), a solver path
+(auto / lds / general) and a workload (SURVEY 8d distributions with random tilt, residual scale,
+randomized gait or a random flight / single-support override), runs it through the C-ABI and the
+oracle on the same inputs, and checks every env:
+  * u0 (the controller's output) within 1e-4 relative (north_star);
+  * x, s, z, y within the parity tests' tolerance for K (SOLVER_CASES: 1e-10 / 1e-9 / 1e-7 / 1e-5 at
+    K <= 1 / 5 / 10 / more);
+  an env outside either bound passes only within 4x its own FP64 floor -- the distance between the two
+  CPU restatements (sparse LDL^T oracle, dense LU) on that env, per output and for u0 -- counted as
+  "floor"; otherwise it is a failure.
+One JSON line per case on stdout (progress), the summary in OUT_JSON. Test infrastructure: the oracle is
+the checker only.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from biped_pympc_amd import _native, solver  # noqa: E402
+from biped_pympc_amd.utils.synthetic import make_workload, solver_init  # noqa: E402
+from oracle import oracle  # noqa: E402
+from tests._util import rel_err_rows  # noqa: E402
+
+
+MAX_FLOOR = 6
+REFINE = os.environ.get("FUZZ_REFINE", "adaptive")  # _native.refinement mode of the HIP calls
+
+
+def floor_env(N, K, ins, e):
+    """tests/_util.py dense_floor_env plus the u0 slice: the relative distance between the two CPU
+    restatements (sparse LDL^T oracle, dense-LU oracle/pdipm_dense.py) for x, s, z, y and u0 of env e."""
+    from oracle.pdipm_dense import pdipm_dense
+    one = [np.asarray(a)[e:e + 1] for a in ins]
+    ref = oracle.pdipm(N, K, one)
+    den = pdipm_dense(N, K, *[a[0] for a in one])
+    fl = [float(rel_err_rows(np.asarray(den[k])[None], ref[k]).max()) for k in range(4)]
+    u = slice(12 * N, 12 * N + 12)
+    fl.append(float(rel_err_rows(np.asarray(den[0])[None, u], ref[0][:, u]).max()))
+    return fl
+
+
+def tol_for(K):
+    return 1e-10 if K <= 1 else 1e-9 if K <= 5 else 1e-7 if K <= 10 else 1e-5
+
+
+def cuda(arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def draw(rng):
+    N = int(rng.integers(1, 33))
+    K = int(rng.integers(1, 26))
+    B = int(rng.integers(1, 301))
+    entry = str(rng.choice(["fused", "cold", "warm"]))
+    path = str(rng.choice(["auto", "auto", "lds", "general"]))
+    kw = dict(tilt=float(rng.uniform(0.0, 0.5)), residuals=bool(rng.integers(0, 2)),
+              residual_scale=float(rng.uniform(0.1, 2.0)), random_gait=bool(rng.integers(0, 2)))
+    if rng.random() < 0.2:  # a contact override: flight or single support over the whole horizon
+        c = np.zeros((B, N, 2), np.int32)
+        c[:, :, 0] = int(rng.integers(0, 2))
+        c[:, :, 1] = int(rng.integers(0, 2))
+        kw["contact_override"] = c
+        kw["random_gait"] = False
+    y0 = float(rng.integers(0, 2))
+    return N, K, B, entry, path, kw, y0
+
+
+def run_case(seed, rng):
+    N, K, B, entry, path, kw, y0 = draw(rng)
+    wl = make_workload(B, N, seed=seed, **kw)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    K0 = 0
+    if entry == "fused":
+        ref = oracle.mpc_solve(N, K, wl.inputs, y0=y0)
+        with _native.solver_path(path), _native.refinement(REFINE):
+            got = solver.mpc_solve(cuda(wl.inputs), N, K, y0=y0)
+        ins = [H, G, A, f, d, b, *solver_init(d, N, y0)]
+    else:
+        it = list(solver_init(d, N, y0))
+        if entry == "warm":
+            K0 = int(rng.integers(1, 11))
+            it = oracle.pdipm(N, K0, [H, G, A, f, d, b, *it])[:4]
+        ins = [H, G, A, f, d, b, *it]
+        ref = oracle.pdipm(N, K, ins)
+        with _native.solver_path(path), _native.refinement(REFINE):
+            got = solver.pdipm(cuda([H, G, A, f, d, b]), cuda(it), N, K)
+    torch.cuda.synchronize()
+    got = [t.cpu().numpy() for t in got]
+    u_err = rel_err_rows(got[0][:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]) if N >= 1 else np.zeros(B)
+    tol = tol_for(K)
+    errs = np.stack([rel_err_rows(got[k], ref[k]) for k in range(4)], 1)  # (B, 4)
+    # per env: x, s, z, y within tol (else within 4x the env's FP64 floor), u0 within 1e-4 (else
+    # within 4x its u0 floor: an ill-posed env where the two CPU restatements themselves disagree)
+    floor_envs, fails = 0, []
+    bad = (errs > tol).any(1) | (u_err > 1e-4)
+    above = np.flatnonzero(bad)
+    # the FP64 floor is a dense-LU solve per env (seconds at N = 32): the worst MAX_FLOOR envs are
+    # checked against it, the rest only counted
+    score = np.maximum((errs[above] / tol).max(1), u_err[above] / 1e-4)
+    above = above[np.argsort(-score)]
+    unchecked = int(max(0, len(above) - MAX_FLOOR))
+    u0_fails = 0
+    for e in above[:MAX_FLOOR]:
+        fl = floor_env(N, K, ins, int(e))
+        ok_x = all(errs[e, k] <= max(tol, 4.0 * fl[k]) for k in range(4))
+        ok_u = u_err[e] <= max(1e-4, 4.0 * fl[4])
+        if ok_x and ok_u:
+            floor_envs += 1
+        else:
+            u0_fails += not ok_u
+            fails.append({"env": int(e), "err": errs[e].tolist(), "u0_err": float(u_err[e]), "floor": fl})
+    finite = all(np.all(np.isfinite(g)) for g in got)
+    case = {"seed": seed, "N": N, "K": K, "B": B, "entry": entry, "K0": K0, "path": path, "y0": y0,
+            "tilt": round(kw["tilt"], 3), "residuals": kw["residuals"], "random_gait": kw["random_gait"],
+            "override": "contact_override" in kw, "max_err": float(errs.max()), "tol": tol,
+            "max_u0_rel": float(u_err.max()), "floor_envs": floor_envs, "above_tol_unchecked": unchecked,
+            "fails": fails[:3],
+            "u0_fails": u0_fails, "finite": bool(finite)}
+    case["ok"] = not fails and finite
+    return case
+
+
+def main():
+    budget = float(sys.argv[1]) if len(sys.argv) > 1 else 150.0
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "parity_fuzz.json")
+    rng = np.random.default_rng(20261018)
+    t0, cases = time.time(), []
+    seed = 50000
+    max_cases = int(os.environ.get("FUZZ_CASES", "0"))  # a fixed case list (A/B of two libraries)
+    while (len(cases) < max_cases) if max_cases else (time.time() - t0 < budget):
+        try:
+            c = run_case(seed, rng)
+        except FloatingPointError as ex:  # the checker's own LDL failed (oracle status): no verdict
+            c = {"seed": seed, "oracle_failed": str(ex), "ok": True, "B": 0, "N": 0, "K": 0, "entry": "-",
+                 "path": "-", "max_u0_rel": 0.0, "floor_envs": 0}
+        cases.append(c)
+        print(json.dumps(c), flush=True)
+        seed += 1
+    summary = {
+        "cases": len(cases), "envs": int(sum(c["B"] for c in cases)),
+        "failed_cases": [c for c in cases if not c["ok"]],
+        "floor_explained_envs": int(sum(c["floor_envs"] for c in cases)),
+        "above_tol_unchecked_envs": int(sum(c.get("above_tol_unchecked", 0) for c in cases)),
+        "oracle_failed_cases": int(sum("oracle_failed" in c for c in cases)),
+        "max_u0_rel": max(c["max_u0_rel"] for c in cases),
+        "horizons": sorted({c["N"] for c in cases if c["N"]}), "iterations": sorted({c["K"] for c in cases if c["K"]}),
+        "by_entry": {e: sum(c["entry"] == e for c in cases) for e in ("fused", "cold", "warm")},
+        "by_path": {p: sum(c["path"] == p for c in cases) for p in ("auto", "lds", "general")},
+        "seconds": round(time.time() - t0, 1), "build_id": _native.build_id(), "refinement": REFINE,
+    }
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as fh:
+        json.dump({"summary": summary, "cases": cases}, fh, indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "failed_cases"} | {"n_failed": len(summary["failed_cases"])}))
+    return 1 if summary["failed_cases"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

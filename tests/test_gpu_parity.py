@@ -528,6 +528,63 @@ def test_batches_past_32_bit_element_offsets(fused, reps):
     torch.cuda.empty_cache()
 
 
+def _tol_for(K):  # SOLVER_CASES extended to every K (scripts/parity_fuzz.py)
+    return 1e-10 if K <= 1 else 1e-9 if K <= 5 else 1e-7 if K <= 10 else 1e-5
+
+
+@pytest.mark.parametrize("mode", ["adaptive", "every_iteration"])
+def test_fuzz_regressions(mode):
+    """Envs the randomised parity campaign (scripts/parity_fuzz.py) found off the reference's trajectory
+    on the register kernels (tests/golden/fuzz_regressions.npz, make_fuzz_regressions.py). Group
+    "adaptive": ill-conditioned iterates (W = z / s of 4.5e3 .. 1.2e8, some with every s above the 1e-8
+    clamp) that drifted 1e2 .. 1e6 x the FP64 floor before the predictor was refined there; the default
+    mode must hold them within 4x their floor. Group "strict": envs 5 .. 400 x the floor in the adaptive
+    mode, at the floor when every iteration refines its predictor (srbd_set_refinement(1)). Per output
+    x, s, z, y: max(the K tolerance, 4 x floor); u0: max(U0_TOL, 4 x its floor)."""
+    from biped_pympc_amd import _native
+    z = np.load(os.path.join(GOLDEN, "fuzz_regressions.npz"))
+    groups = ("adaptive",) if mode == "adaptive" else ("adaptive", "strict")
+    keys = sorted({k.split("_")[0] for k in z.files if k.startswith(groups)})
+    assert len(keys) == (8 if mode == "adaptive" else 15)
+    for key in keys:
+        N, K, seed, env = (int(v) for v in z[f"{key}_NK"])
+        ins = [z[f"{key}_in{j}"][None] for j in range(10)]
+        with _native.refinement(mode):
+            out = solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K)
+            torch.cuda.synchronize()
+        floor = z[f"{key}_floor"]
+        for j in range(4):
+            e = rel_err_rows(out[j].cpu().numpy(), z[f"{key}_ref{j}"][None])[0]
+            assert e <= max(_tol_for(K), 4.0 * floor[j]), (key, seed, env, j, e, floor[j])
+        u = slice(12 * N, 12 * N + 12)
+        eu = rel_err_rows(out[0].cpu().numpy()[:, u], z[f"{key}_ref0"][None, u])[0]
+        assert eu <= max(U0_TOL, 4.0 * floor[4]), (key, seed, env, "u0", eu, floor[4])
+    assert _native.current_refinement() == 0
+
+
+def test_refinement_mode_is_per_call_and_exact():
+    """Both refinement modes on the benchmark workload agree within the K = 10 tolerance, the mode
+    reaches the fused step and the CCS solver (every_iteration changes bits), and the default restores."""
+    from biped_pympc_amd import _native
+    N, K, B = 10, 10, 300
+    wl = make_workload(B, N, seed=4242)
+    ins = _cuda(wl.inputs)
+    a = [t.clone() for t in solver.mpc_solve(ins, N, K)]
+    with _native.refinement("every_iteration"):
+        assert _native.current_refinement() == 1
+        b = [t.clone() for t in solver.mpc_solve(ins, N, K)]
+    c = solver.mpc_solve(ins, N, K)
+    torch.cuda.synchronize()
+    assert all(torch.equal(x, y) for x, y in zip(a, c))
+    assert not torch.equal(a[2], b[2])
+    ref = oracle.mpc_solve(N, K, wl.inputs)
+    for k in range(4):
+        assert rel_err_rows(a[k].cpu().numpy(), ref[k]).max() <= dict(SOLVER_CASES)[K]
+        assert rel_err_rows(b[k].cpu().numpy(), ref[k]).max() <= dict(SOLVER_CASES)[K]
+    with pytest.raises(RuntimeError):
+        _native.check(_native.lib().srbd_set_refinement(2), "srbd_set_refinement")
+
+
 def test_empty_batch_is_a_no_op():
     N = 10
     wl = make_workload(1, N, seed=1)
