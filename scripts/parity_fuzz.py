@@ -7,7 +7,8 @@
 
 Each case draws a horizon N in 1..32, an iteration count K in 1..25, a batch B in 1..300, an entry
 (fused step with y0 in {0, 1}; the solver from the GPU caller's cold init; the solver warm-started
-from the oracle's iterate after K0 iterations -- the reference caller's chained calls), a solver path
+from the oracle's iterate after K0 iterations -- the reference caller's chained calls; with FUZZ_CCS=1
+also the reference's _ccs entry from a random x_init), a solver path
 (auto / lds / general) and a workload (SURVEY 8d distributions with random tilt, residual scale,
 randomized gait or a random flight / single-support override), runs it through the C-ABI and the
 oracle on the same inputs, and checks every env:
@@ -38,6 +39,10 @@ from tests._util import rel_err_rows  # noqa: E402
 
 MAX_FLOOR = 6
 REFINE = os.environ.get("FUZZ_REFINE", "adaptive")  # _native.refinement mode of the HIP calls
+# FUZZ_CCS=1 adds the reference's _ccs entry (x from x_init, s = max(h - G x, 1), z = 1, y = 0;
+# srbd_pdipm_ccs) to the draw -- a different random sequence from the default one, which
+# tests/golden/make_fuzz_regressions.py replays
+ENTRIES = ["fused", "cold", "warm"] + (["ccs"] if os.environ.get("FUZZ_CCS") == "1" else [])
 
 
 def floor_env(N, K, ins, e):
@@ -65,7 +70,7 @@ def draw(rng):
     N = int(rng.integers(1, 33))
     K = int(rng.integers(1, 26))
     B = int(rng.integers(1, 301))
-    entry = str(rng.choice(["fused", "cold", "warm"]))
+    entry = str(rng.choice(ENTRIES))
     path = str(rng.choice(["auto", "auto", "lds", "general"]))
     kw = dict(tilt=float(rng.uniform(0.0, 0.5)), residuals=bool(rng.integers(0, 2)),
               residual_scale=float(rng.uniform(0.1, 2.0)), random_gait=bool(rng.integers(0, 2)))
@@ -79,25 +84,59 @@ def draw(rng):
     return N, K, B, entry, path, kw, y0
 
 
-def run_case(seed, rng):
+def draw_case(rng):
+    """draw() plus the entry's own draws, in the order the campaign consumes the generator."""
     N, K, B, entry, path, kw, y0 = draw(rng)
+    extra = {}
+    if entry == "ccs":
+        extra["scale"] = float(rng.uniform(0.1, 5.0))
+    elif entry == "warm":
+        extra["K0"] = int(rng.integers(1, 11))
+    return N, K, B, entry, path, kw, y0, extra
+
+
+def replay(seed_want):
+    """The campaign's case `seed_want` (seeds count from 50000 in draw order)."""
+    rng = np.random.default_rng(20261018)
+    for seed in range(50000, seed_want + 1):
+        case = draw_case(rng)
+    return case
+
+
+def case_inputs(seed, N, K, B, entry, kw, y0, extra):
+    """The case's workload and solver inputs [H, G, A, f, d, b, x, s, z, y] (the start of its iterations)."""
     wl = make_workload(B, N, seed=seed, **kw)
     H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
-    K0 = 0
-    if entry == "fused":
-        ref = oracle.mpc_solve(N, K, wl.inputs, y0=y0)
-        with _native.solver_path(path), _native.refinement(REFINE):
-            got = solver.mpc_solve(cuda(wl.inputs), N, K, y0=y0)
-        ins = [H, G, A, f, d, b, *solver_init(d, N, y0)]
+    if entry == "ccs":
+        from biped_pympc_amd import layout
+        dims = layout.Dims(N)
+        x0 = np.random.default_rng(seed).normal(0.0, extra["scale"], (B, dims.nz))
+        Gd = layout.to_dense(G, *layout.ccs_G(N), (dims.n_ineq, dims.nz))
+        s0 = np.maximum(d - np.einsum("bij,bj->bi", Gd, x0), 1.0)
+        it = [x0, s0, np.ones((B, dims.n_ineq)), np.zeros((B, dims.n_eq))]
     else:
         it = list(solver_init(d, N, y0))
         if entry == "warm":
-            K0 = int(rng.integers(1, 11))
-            it = oracle.pdipm(N, K0, [H, G, A, f, d, b, *it])[:4]
-        ins = [H, G, A, f, d, b, *it]
-        ref = oracle.pdipm(N, K, ins)
-        with _native.solver_path(path), _native.refinement(REFINE):
-            got = solver.pdipm(cuda([H, G, A, f, d, b]), cuda(it), N, K)
+            it = oracle.pdipm(N, extra["K0"], [H, G, A, f, d, b, *it])[:4]
+    return wl, [H, G, A, f, d, b, *it]
+
+
+def hip_solve(N, K, entry, path, y0, wl, ins):
+    """The case's HIP call: fused step, srbd_pdipm_ccs, or srbd_pdipm from the given iterate."""
+    with _native.solver_path(path), _native.refinement(REFINE):
+        if entry == "fused":
+            return solver.mpc_solve(cuda(wl.inputs), N, K, y0=y0)
+        if entry == "ccs":
+            return solver.pdipm_ccs(cuda(ins[:6]), cuda([ins[6]])[0], N, K)
+        return solver.pdipm(cuda(ins[:6]), cuda(ins[6:]), N, K)
+
+
+def run_case(seed, rng):
+    N, K, B, entry, path, kw, y0, extra = draw_case(rng)
+    K0 = extra.get("K0", 0)
+    wl, ins = case_inputs(seed, N, K, B, entry, kw, y0, extra)
+    ref = oracle.mpc_solve(N, K, wl.inputs, y0=y0) if entry == "fused" else oracle.pdipm(N, K, ins)
+    got = hip_solve(N, K, entry, path, y0, wl, ins)
     torch.cuda.synchronize()
     got = [t.cpu().numpy() for t in got]
     u_err = rel_err_rows(got[0][:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]) if N >= 1 else np.zeros(B)
@@ -158,7 +197,7 @@ def main():
         "oracle_failed_cases": int(sum("oracle_failed" in c for c in cases)),
         "max_u0_rel": max(c["max_u0_rel"] for c in cases),
         "horizons": sorted({c["N"] for c in cases if c["N"]}), "iterations": sorted({c["K"] for c in cases if c["K"]}),
-        "by_entry": {e: sum(c["entry"] == e for c in cases) for e in ("fused", "cold", "warm")},
+        "by_entry": {e: sum(c["entry"] == e for c in cases) for e in ENTRIES},
         "by_path": {p: sum(c["path"] == p for c in cases) for p in ("auto", "lds", "general")},
         "seconds": round(time.time() - t0, 1), "build_id": _native.build_id(), "refinement": REFINE,
     }

@@ -25,7 +25,6 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import numpy as np  # noqa: E402
 
 import parity_fuzz as pf  # noqa: E402
-from biped_pympc_amd.utils.synthetic import make_workload, solver_init  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 # (seed, env) of the campaign's failing envs (profiles/r05/parity_fuzz.txt)
@@ -34,29 +33,13 @@ ADAPTIVE = [(51078, 139), (50301, 189), (50690, 61), (50067, 180), (50167, 55), 
 STRICT = [(50758, 116), (50870, 51), (51078, 182), (50814, 129), (50944, 98), (50824, 2), (50055, 231)]
 
 
-def replay(seed_want):
-    """The campaign's case `seed_want`: its draw, with the rng advanced exactly as parity_fuzz does."""
-    rng = np.random.default_rng(20261018)
-    seed = 50000
-    while True:
-        N, K, B, entry, path, kw, y0 = pf.draw(rng)
-        K0 = int(rng.integers(1, 11)) if entry == "warm" else 0
-        if seed == seed_want:
-            return N, K, B, entry, kw, y0, K0
-        seed += 1
-
-
 def main():
     out = {}
     for group, pairs in (("adaptive", ADAPTIVE), ("strict", STRICT)):
         for i, (seed, env) in enumerate(pairs):
-            N, K, B, entry, kw, y0, K0 = replay(seed)
-            wl = make_workload(B, N, seed=seed, **kw)
-            H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
-            it = list(solver_init(d, N, y0))
-            if entry == "warm":
-                it = oracle.pdipm(N, K0, [H, G, A, f, d, b, *it])[:4]
-            ins = [np.ascontiguousarray(a[env:env + 1]) for a in (H, G, A, f, d, b, *it)]
+            N, K, B, entry, path, kw, y0, extra = pf.replay(seed)
+            _, ins = pf.case_inputs(seed, N, K, B, entry, kw, y0, extra)
+            ins = [np.ascontiguousarray(a[env:env + 1]) for a in ins]
             ref = oracle.pdipm(N, K, ins)
             floor = pf.floor_env(N, K, ins, 0)
             key = f"{group}{i}"
@@ -67,6 +50,7 @@ def main():
                 out[f"{key}_ref{j}"] = ref[j][0]
             out[f"{key}_floor"] = np.array(floor)
             print(key, seed, env, N, K, entry, ["%.1e" % v for v in floor])
+    assert "ccs" not in pf.ENTRIES  # the default campaign's sequence (FUZZ_CCS unset)
     np.savez_compressed(os.path.join(HERE, "fuzz_regressions.npz"), **out)
 
 
