@@ -171,6 +171,67 @@ __device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
   for (int e = 0; e < n * (n + 1) / 2; ++e) a[e] = -a[e];
 }
 
+// LDL^T of a packed symmetric positive definite block (lower packed, sym_idx order), no pivoting
+// (backward stable for SPD): on return the diagonal slots hold 1 / d_j, the others L_ij. Used where a
+// solve must keep the stiff direction: Phi_f reaches cond ~1e12 as the barrier sharpens, and an
+// explicit inverse applied to a vector loses the component along G_i (error ~cond x that of a stable
+// solve) that Lambda ~ W then multiplies into dz (scripts/stiff_dz_emu.py).
+template <int n>
+__device__ inline void ldlt_factor(double (&a)[n * (n + 1) / 2]) {
+  double d[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    double dj = a[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) dj -= a[j * (j + 1) / 2 + k] * a[j * (j + 1) / 2 + k] * d[k];
+    d[j] = dj;
+    const double id = rcp3(dj);
+#pragma unroll
+    for (int i = j + 1; i < n; ++i) {
+      double v = a[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= a[i * (i + 1) / 2 + k] * a[j * (j + 1) / 2 + k] * d[k];
+      a[i * (i + 1) / 2 + j] = v * id;
+    }
+    a[j * (j + 1) / 2 + j] = id;
+  }
+}
+// x = A^-1 v from ldlt_factor's packed factors at f (LDS or registers)
+template <int n>
+__device__ inline void ldlt_solve_p(const double* f, const double (&v)[n], double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    double y = v[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) y -= f[i * (i + 1) / 2 + k] * x[k];
+    x[i] = y;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) x[i] *= f[i * (i + 1) / 2 + i];
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) x[i] -= f[k * (k + 1) / 2 + i] * x[k];
+  }
+}
+template <int n>
+__device__ inline void ldlt_solve(const double (&f)[n * (n + 1) / 2], const double (&v)[n], double (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    double y = v[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) y -= f[i * (i + 1) / 2 + k] * x[k];
+    x[i] = y;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) x[i] *= f[i * (i + 1) / 2 + i];
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) x[i] -= f[k * (k + 1) / 2 + i] * x[k];
+  }
+}
+
 // (G x)_q of inequality row q from the stage's 28 CCS values of G (c_tab.grow / gcol) and the u
 // part xu of x, each product rounded: the reference's G_mat @ x_init (sparse_pdipm_solver.py:31);
 // a row holds at most two nonzeros, so every summation order gives this value.
@@ -442,7 +503,7 @@ struct SolverCtx {
           for (int c = 0; c <= r; ++c)
             if ((nzm >> r) & (nzm >> c) & 1) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
       }
-      sweep_inverse<4>(a);
+      ldlt_factor<4>(a);  // every use of Phi_f^-1 is a stable solve with these factors
 #pragma unroll
       for (int e = 0; e < 10; ++e) PH[24 * i + 10 * f + e] = a[e];
       } else {
@@ -470,14 +531,10 @@ struct SolverCtx {
           vr[a] = Nv(i, r, T->foot_col[f][a]);
           vc[a] = Nv(i, c, T->foot_col[f][a]);
         }
-        const double* ph = PH + 24 * i + 10 * f;
+        double pv[4];
+        ldlt_solve_p<4>(PH + 24 * i + 10 * f, vc, pv);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * vc[b];
-          v += vr[a] * t;
-        }
+        for (int a = 0; a < 4; ++a) v += vr[a] * pv[a];
       }
       v += Nv(i, r, 6) * Nv(i, c, 6) * PH[24 * i + 20] + Nv(i, r, 9) * Nv(i, c, 9) * PH[24 * i + 21] +
            Nv(i, r, 8) * Nv(i, c, 8) * PH[24 * i + 22] + Nv(i, r, 11) * Nv(i, c, 11) * PH[24 * i + 23];
@@ -678,17 +735,12 @@ struct SolverCtx {
     for (int task = lane; task < 3 * N; task += nt) {
       if (task < 2 * N) {
       const int i = task >> 1, f = task & 1;
-      const double* ph = PH + 24 * i + 10 * f;
-      double rv[4];
+      double rv[4], tv[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) rv[a] = R1T[12 * N + 12 * i + T->foot_col[f][a]];
+      ldlt_solve_p<4>(PH + 24 * i + 10 * f, rv, tv);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double t = 0.0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * rv[b];
-        TV[12 * N + 12 * i + T->foot_col[f][a]] = t;
-      }
+      for (int a = 0; a < 4; ++a) TV[12 * N + 12 * i + T->foot_col[f][a]] = tv[a];
       } else {
       const int i = task - 2 * N;
       const int b = 12 * N + 12 * i;
@@ -845,17 +897,14 @@ struct SolverCtx {
       auto aty_u = [&](int j) { return WV[12 * i + j]; };
       if (foot) {
         const int f = task & 1;
-        const double* ph = PH + 24 * i + 10 * f;
-        double av[4];
+        double av[4], tv[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) av[a] = aty_u(T->foot_col[f][a]);
+        ldlt_solve_p<4>(PH + 24 * i + 10 * f, av, tv);
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
           const int o = b + T->foot_col[f][a];
-          TV[o] = ref ? xsg[o] + (TV[o] - t) : TV[o] - t;
+          TV[o] = ref ? xsg[o] + (TV[o] - tv[a]) : TV[o] - tv[a];
         }
       } else {
         const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);

@@ -171,7 +171,7 @@ struct FastCtx {
 #pragma unroll
           for (int c = 0; c <= r; ++c) a[r * (r + 1) / 2 + c] += lam * g4[r] * g4[c];
       }
-      sweep_inverse<4>(a);
+      ldlt_factor<4>(a);  // every use of Phi_f^-1 is a stable solve with these factors
 #pragma unroll
       for (int e = 0; e < 10; ++e) PH[20 * i + 10 * f + e] = a[e];
     }
@@ -183,20 +183,15 @@ struct FastCtx {
       double v = (i == 0 ? K0 : K1)[l];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        const double* ph = PH + 20 * i + 10 * f;
-        double vc[4], vr[4];
+        double vc[4], vr[4], pv[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           vr[a] = Nd[r * 12 + c_tab.foot_col[f][a]];
           vc[a] = Nd[c * 12 + c_tab.foot_col[f][a]];
         }
+        ldlt_solve_p<4>(PH + 20 * i + 10 * f, vc, pv);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) t += ph[sym_idx(a, b)] * vc[b];
-          v += vr[a] * t;
-        }
+        for (int a = 0; a < 4; ++a) v += vr[a] * pv[a];
       }
       DV[e] = v;
     }
@@ -387,9 +382,8 @@ struct FastCtx {
     for (int task = lane; task < 3 * N; task += 64) {
       if (task < 2 * N) {
         const int i = task >> 1, f = task & 1, b = 12 * N + 12 * i;
-        const double* ph = PH + 20 * i + 10 * f;
         const double* vv = VV + 16 * i + 8 * f;
-        double rv[4];
+        double rv[4], tv[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           const int col = c_tab.foot_col[f][a];
@@ -400,13 +394,9 @@ struct FastCtx {
           }
           rv[a] = -RX[b + col] - gv;
         }
+        ldlt_solve_p<4>(PH + 20 * i + 10 * f, rv, tv);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * rv[q];
-          TV[b + c_tab.foot_col[f][a]] = t;
-        }
+        for (int a = 0; a < 4; ++a) TV[b + c_tab.foot_col[f][a]] = tv[a];
       } else {
         const int i = task - 2 * N, b = 12 * N + 12 * i;
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
@@ -536,17 +526,14 @@ struct FastCtx {
       const double* yi = QV + 12 * i;
       if (foot) {
         const int f = task & 1;
-        const double* ph = PH + 20 * i + 10 * f;
-        double av[4];
+        double av[4], tv[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) av[a] = dotcol12(Nd, c_tab.foot_col[f][a], yi);
+        ldlt_solve_p<4>(PH + 20 * i + 10 * f, av, tv);
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t += ph[sym_idx(a, q)] * av[q];
           const int o = b + c_tab.foot_col[f][a];
-          TV[o] = ref ? xsg[o] + (TV[o] - t) : TV[o] - t;
+          TV[o] = ref ? xsg[o] + (TV[o] - tv[a]) : TV[o] - tv[a];
         }
       } else {
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];

@@ -681,11 +681,39 @@ struct RegCtx {
         else a[8] += lam * go * gz;            // (my, fz)
       }
     }
-    sweep_inverse<4>(a);  // IEEE pivots: Phi_f reaches cond ~1e7 as the barrier sharpens
+    // LDL^T factors for the solves (ph: phi_solve) and, from them, the inverse for the S_ii build (dst):
+    // the Schur complement and the solves take the same Phi_f^-1 (a mismatched pair -- the sweep
+    // inverse in S_ii, stable solves in dx -- left z 1e-4 off at K = 20)
+    ldlt_factor<4>(a);
 #pragma unroll
-    for (int e = 0; e < 10; ++e) {
-      if constexpr (!kPipe) ph[e] = a[e];
-      dst[20 * i + 10 * f + e] = a[e];
+    for (int c = 0; c < 4; ++c) {
+      double ec[4] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0, c == 3 ? 1.0 : 0.0}, pc[4];
+      ldlt_solve<4>(a, ec, pc);
+#pragma unroll
+      for (int r = c; r < 4; ++r) dst[20 * i + 10 * f + r * (r + 1) / 2 + c] = pc[r];
+    }
+    if constexpr (!kPipe) {
+#pragma unroll
+      for (int e = 0; e < 10; ++e) ph[e] = a[e];
+    }
+  }
+  // x = Phi_f^-1 v for foot task fl, by a stable solve with the lane's LDL^T factors: the explicit
+  // inverse applied to v loses the stiff direction G_i dx of rows with W = z / s ~ 1e7..1e8, whose error
+  // Lambda ~ W multiplies into dz. The pipelined variant (kPipe, off) multiplies by the
+  // inverse it keeps in LDS.
+  __device__ void phi_solve(int fl, const double (&v)[4], double (&x)[4]) const {
+    if constexpr (kPipe) {
+      double P[10];
+      load_ph(fl, P);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * v[q];
+        x[a] = t;
+      }
+    } else {
+      ldlt_solve<4>(ph, v, x);
     }
   }
 
@@ -1171,21 +1199,16 @@ struct RegCtx {
         }
         gt[2] = gz0 + gz1;
       }
-      double e1[4], P[10];
-      load_ph(fl, P);
+      double e1[4], c[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         const int j = foot_colj(f, a);
         const double ay = a < 3 ? ncol(Nd, j, QV + b, a) : ncol<false>(Nd, j, QV + b, 0);
         e1[a] = ((-RXu[b + j] - (Hu[j] + kBeta) * TV[nx + b + j]) - gt[a]) - ay;
       }
+      phi_solve(fl, e1, c);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * e1[q];
-        TV[nx + b + foot_colj(f, a)] += t;
-      }
+      for (int a = 0; a < 4; ++a) TV[nx + b + foot_colj(f, a)] += c[a];
     }
     qp_sync<TPB>();
     if (kAff) {  // Z is dead from here on: it keeps e3 for solve_finish<true, true>
@@ -1245,8 +1268,7 @@ struct RegCtx {
     if ((unsigned)fl < (unsigned)(((kMode == 0 || rx) ? 3 : 2) * N)) {
       if (fl < 2 * N) {
         const int i = fl >> 1, f = fl & 1, b = 12 * i;
-        double rv[4], P[10];
-        load_ph(fl, P);
+        double rv[4], tv[4];
         {
           const double* vv = VV + 16 * i + 8 * f;
           const double* g = Gf + g_row(8 * f);  // (G^T vv)_a over column a's structural rows
@@ -1267,13 +1289,9 @@ struct RegCtx {
           rv[2] = -RXu[b + foot_colj(f, 2)] - (gz0 + gz1);
           rv[3] = -RXu[b + foot_colj(f, 3)] - gmy;
         }
+        phi_solve(fl, rv, tv);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * rv[q];
-          TV[nx + b + foot_colj(f, a)] = t;
-        }
+        for (int a = 0; a < 4; ++a) TV[nx + b + foot_colj(f, a)] = tv[a];
       } else {
         const int i = fl - 2 * N, b = 12 * i;
         const double r4a = -REm[2 * i], r4b = -REm[2 * i + 1];
@@ -1403,18 +1421,15 @@ struct RegCtx {
       const double* yi = QV + 12 * i;
       if (foot) {
         const int f = fl & 1;
-        double av[4], P[10];
-        load_ph(fl, P);
+        double av[4], tv[4];
 #pragma unroll
         for (int a = 0; a < 3; ++a) av[a] = ncol(Nd, foot_colj(f, a), yi, a);
         av[3] = ncol<false>(Nd, foot_colj(f, 3), yi, 0);
+        phi_solve(fl, av, tv);
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * av[q];
           const int o = b + foot_colj(f, a);
-          TV[o] = TV[o] - t;
+          TV[o] = TV[o] - tv[a];
         }
       } else {
         const double r4a = kRefine ? 0.0 : -REm[2 * i], r4b = kRefine ? 0.0 : -REm[2 * i + 1];

@@ -66,10 +66,11 @@ def main(seed, env, K):
         sol = sol + sl.lu_solve(lu, (rl - Kl @ sol.astype(np.longdouble)).astype(np.float64))
     dz_ref = sol[nz + m:nz + 2 * m]
     PhiS = sweep_inv(Phi)
-    S = A @ np.linalg.solve(Phi, A.T) + DELTA * np.eye(p)   # the dual Schur solve itself exact here
-    lus = sl.lu_factor(S)
+    S = A @ np.linalg.solve(Phi, A.T) + DELTA * np.eye(p)   # the dual Schur complement from an exact Phi solve
+    S_sweep = A @ PhiS @ A.T + DELTA * np.eye(p)            # ... and from the sweep inverse (as the kernels)
+    lus_exact, lus_sweep = sl.lu_factor(S), sl.lu_factor(S_sweep)
 
-    def reduced(phis, steps):
+    def reduced(phis, steps, lus):
         g = A @ phis(r1t) - r4
         yy = sl.lu_solve(lus, g)
         dx = phis(r1t - A.T @ yy)
@@ -85,11 +86,16 @@ def main(seed, env, K):
     hi = W > 1e6
     print(f"seed {seed} env {env} N={N} iteration {K}: max W {W.max():.1e}, rows with W > 1e6: {int(hi.sum())}, "
           f"cond Phi {np.linalg.cond(Phi):.1e}")
-    for name, phis in (("explicit inverse (kernels)", lambda v: PhiS @ v), ("LU solve of Phi", lambda v: np.linalg.solve(Phi, v))):
+    lu_phi = sl.lu_factor(Phi)
+    variants = (("explicit inverse, exact S", lambda v: PhiS @ v, lus_exact),
+                ("LU solve of Phi, exact S", lambda v: sl.lu_solve(lu_phi, v), lus_exact),
+                ("explicit inverse, sweep S", lambda v: PhiS @ v, lus_sweep),
+                ("LU solve of Phi, sweep S", lambda v: sl.lu_solve(lu_phi, v), lus_sweep))
+    for name, phis, lus in variants:
         for steps in (0, 1, 2):
-            dz = reduced(phis, steps)
+            dz = reduced(phis, steps, lus)
             err = np.abs(dz - dz_ref) / sc
-            print(f"  {name:28s} refinement steps {steps}: dz rel err max {err.max():.1e}, at W > 1e6 rows "
+            print(f"  {name:30s} refinement steps {steps}: dz rel err max {err.max():.1e}, at W > 1e6 rows "
                   f"{err[hi].max() if hi.any() else 0:.1e}, elsewhere {err[~hi].max():.1e}")
 
 
