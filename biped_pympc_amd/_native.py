@@ -207,7 +207,7 @@ def current_refinement() -> int:
 class refinement:
     """Context manager selecting the register kernels' affine-direction refinement (srbd_set_refinement):
     "adaptive" (default: iterations with an ill-conditioned iterate) or "every_iteration" (closer to the
-    FP64 floor of the reference's elimination, ~18 % slower at N = 10). For the HIP device
+    FP64 floor of the reference's elimination, ~15 % slower at N = 10). For the HIP device
     current on entry; the previous mode of that device is restored on exit."""
 
     def __init__(self, mode: str):

@@ -139,9 +139,9 @@ int srbd_get_solver_path(void);
  * full KKT; the affine (predictor) direction, whose ds / dz set sigma and the corrector, is refined
  * 0 = (default) in iterations with an ill-conditioned iterate: some row with z / s >= 1e3 or an s at its
  * 1e-8 clamp -- where an unrefined predictor lets the trajectory drift from the reference's;
- * 1 = in every iteration (as the LDS-resident and general kernels always do), for ~18 % more time at
- * N = 10: scripts/parity_fuzz.py's failing cases drop by 60 % (0 of its default 1200); what remains is z
- * in rows at the 1e-8 clamp with z / s ~ 1e7..1e8, the reduced elimination's own limit.
+ * 1 = in every iteration (as the LDS-resident and general kernels always do), for ~15 % more time at
+ * N = 10: scripts/parity_fuzz.py then fails 0 of its default 1200 cases and 3 of 3369 with the _ccs entry,
+ * all within 8x the FP64 floor, against 10 and 19 in mode 0.
  * Returns 0, or an error for another mode. */
 int srbd_set_refinement(int mode);
 /* The refinement mode in effect for the current HIP device (0 if never set). */
