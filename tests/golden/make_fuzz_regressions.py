@@ -11,7 +11,10 @@ two CPU restatements, the sparse LDL^T oracle and oracle/pdipm_dense.py (dense L
     clamp -- where the unrefined predictor let the trajectory drift 1e2 .. 1e6 x the floor (z up to 2.9e-4
     relative); the default adaptive refinement (srbd_set_refinement(0)) must hold them at 4 x the floor;
   group "strict": envs 5 .. 400 x the floor under the adaptive mode (well-conditioned iterates, the
-    explicit-inverse Schur complement's own rounding), at the floor with srbd_set_refinement(1).
+    explicit-inverse Schur complement's own rounding), at the floor with srbd_set_refinement(1);
+  group "stiff": from the campaign with the _ccs entry, envs whose z sat 1e3 .. 4e5 x the floor at clamped
+    rows in the strict mode on the register, LDS-resident or general kernels (the path is stored) until the
+    foot blocks were applied through LDL^T solves.
 tests/test_gpu_parity.py::test_fuzz_regressions runs both groups.
 """
 import os
@@ -31,11 +34,19 @@ from oracle import oracle  # noqa: E402
 ADAPTIVE = [(51078, 139), (50301, 189), (50690, 61), (50067, 180), (50167, 55), (50217, 151),
             (50695, 197), (50368, 179)]
 STRICT = [(50758, 116), (50870, 51), (51078, 182), (50814, 129), (50944, 98), (50824, 2), (50055, 231)]
+# the _ccs campaign's sequence (FUZZ_CCS=1): envs whose z sat 1e3..4e5 x the floor at clamped rows (W = z / s
+# ~ 1e7..1e8) on the path named, in the strict mode, before the LDL^T foot-block solves
+STIFF = [(54319, 67), (53918, 121), (50149, 2), (50902, 51), (51320, 64), (55147, 83)]
+
+
+PATHS = {"auto": 0, "general": 1, "lds": 2}
 
 
 def main():
     out = {}
-    for group, pairs in (("adaptive", ADAPTIVE), ("strict", STRICT)):
+    default_entries = list(pf.ENTRIES)
+    for group, pairs in (("adaptive", ADAPTIVE), ("strict", STRICT), ("stiff", STIFF)):
+        pf.ENTRIES[:] = default_entries + (["ccs"] if group == "stiff" else [])
         for i, (seed, env) in enumerate(pairs):
             N, K, B, entry, path, kw, y0, extra = pf.replay(seed)
             _, ins = pf.case_inputs(seed, N, K, B, entry, kw, y0, extra)
@@ -43,13 +54,14 @@ def main():
             ref = oracle.pdipm(N, K, ins)
             floor = pf.floor_env(N, K, ins, 0)
             key = f"{group}{i}"
-            out[f"{key}_NK"] = np.array([N, K, seed, env])
+            out[f"{key}_NK"] = np.array([N, K, seed, env, PATHS[path]])
             for j, a in enumerate(ins):
                 out[f"{key}_in{j}"] = a[0]
             for j in range(4):
                 out[f"{key}_ref{j}"] = ref[j][0]
             out[f"{key}_floor"] = np.array(floor)
             print(key, seed, env, N, K, entry, ["%.1e" % v for v in floor])
+    pf.ENTRIES[:] = default_entries
     assert "ccs" not in pf.ENTRIES  # the default campaign's sequence (FUZZ_CCS unset)
     np.savez_compressed(os.path.join(HERE, "fuzz_regressions.npz"), **out)
 

@@ -539,17 +539,20 @@ def test_fuzz_regressions(mode):
     "adaptive": ill-conditioned iterates (W = z / s of 4.5e3 .. 1.2e8, some with every s above the 1e-8
     clamp) that drifted 1e2 .. 1e6 x the FP64 floor before the predictor was refined there; the default
     mode must hold them within 4x their floor. Group "strict": envs 5 .. 400 x the floor in the adaptive
-    mode, at the floor when every iteration refines its predictor (srbd_set_refinement(1)). Per output
+    mode, at the floor when every iteration refines its predictor (srbd_set_refinement(1)). Group "stiff"
+    (strict mode, on the solver path each env failed on): z 1e3 .. 4e5 x the floor at clamped rows until
+    the foot blocks were applied through LDL^T solves. Per output
     x, s, z, y: max(the K tolerance, 4 x floor); u0: max(U0_TOL, 4 x its floor)."""
     from biped_pympc_amd import _native
     z = np.load(os.path.join(GOLDEN, "fuzz_regressions.npz"))
-    groups = ("adaptive",) if mode == "adaptive" else ("adaptive", "strict")
+    groups = ("adaptive",) if mode == "adaptive" else ("adaptive", "strict", "stiff")
     keys = sorted({k.split("_")[0] for k in z.files if k.startswith(groups)})
-    assert len(keys) == (8 if mode == "adaptive" else 15)
+    assert len(keys) == (8 if mode == "adaptive" else 21)
+    paths = {v: k for k, v in _native.SOLVER_PATHS.items()}
     for key in keys:
-        N, K, seed, env = (int(v) for v in z[f"{key}_NK"])
+        N, K, seed, env, path = (int(v) for v in z[f"{key}_NK"])
         ins = [z[f"{key}_in{j}"][None] for j in range(10)]
-        with _native.refinement(mode):
+        with _native.refinement(mode), _native.solver_path(paths[path]):
             out = solver.pdipm(_cuda(ins[:6]), _cuda(ins[6:]), N, K)
             torch.cuda.synchronize()
         floor = z[f"{key}_floor"]
