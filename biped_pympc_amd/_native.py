@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
     L.srbd_set_refinement.argtypes = [ctypes.c_int]
     L.srbd_get_refinement.restype = ctypes.c_int
     L.srbd_get_refinement.argtypes = []
+    L.srbd_set_refinement_policy.restype = ctypes.c_int
+    L.srbd_set_refinement_policy.argtypes = [ctypes.c_int, ctypes.c_double]
     L.srbd_pattern_ccs.restype = ctypes.c_int
     L.srbd_pattern_ccs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_int)]
@@ -224,8 +226,48 @@ class refinement:
 
     def __exit__(self, *exc):
         import torch
+        with torch.cuda.device(self._device):  # (an explicit policy before: back to mode 0)
+            check(lib().srbd_set_refinement(self._prev if self._prev in (0, 1) else 0), "srbd_set_refinement")
+
+
+# srbd_set_refinement_policy's word (include/srbd_mpc.h SRBD_REFINE_*)
+REFINE_AFFINE_ALL = 1
+
+
+def refine_affine_first(k: int) -> int:
+    return (int(k) & 255) << 8
+
+
+def refine_affine_last(k: int) -> int:
+    return (int(k) & 255) << 16
+
+
+def refine_combined(c: int) -> int:
+    """0 every iteration, 1 never, 2 the last ceil(K / 2) iterations, 3 the dual rows only."""
+    return (int(c) & 3) << 24
+
+
+class refinement_policy:
+    """Context manager setting an explicit refinement policy (srbd_set_refinement_policy(flags, w)) on the
+    current HIP device -- diagnostics and A/B campaigns (scripts/parity_fuzz.py); on exit the previous
+    mode is restored (a previous explicit policy is not: it returns to its mode 0 / 1 default)."""
+
+    def __init__(self, flags: int, w: float = 1e3):
+        self.flags, self.w = int(flags), float(w)
+        self._prev = None
+        self._device = None
+
+    def __enter__(self):
+        import torch
+        self._device = torch.cuda.current_device()
+        self._prev = current_refinement()
+        check(lib().srbd_set_refinement_policy(self.flags, self.w), "srbd_set_refinement_policy")
+        return self
+
+    def __exit__(self, *exc):
+        import torch
         with torch.cuda.device(self._device):
-            check(lib().srbd_set_refinement(self._prev), "srbd_set_refinement")
+            check(lib().srbd_set_refinement(self._prev if self._prev in (0, 1) else 0), "srbd_set_refinement")
 
 
 def build_id() -> str:

@@ -333,7 +333,8 @@ class GraphedMPCStep:
     between replays. Every replay first compares the storage of every source tensor -- the state
     estimate and command fields, the contact schedule, dt_mpc, the residual accelerations, the
     knot-point state -- with what was captured, and the constants baked into the graph (mass, mu,
-    I_body, Q, R, step dt, layout, iterations, y0): a tensor replaced by assignment
+    I_body, Q, R, step dt, layout, iterations, y0, the device's refinement mode of srbd_set_refinement):
+    a tensor replaced by assignment
     (``data.root_position = ...``, ``c.residual_lin_accel = x.clone()``, a setter) or a changed
     constant makes the replay raise instead of silently reading the captured values. (Q and R given
     as device tensors are compared by storage, not value.)
@@ -384,7 +385,8 @@ class GraphedMPCStep:
         consts = (("mass", c.mass), ("mu", c.mu), ("I_body", value(c.I_body)), ("Q", value(c.Q)),
                   ("R", value(c.R)), ("step_dt", c.cfg.decimation * c.cfg.dt),
                   ("literal_layout", c.cfg.literal_layout), ("pdipm_iterations", c.cfg.pdipm_iterations),
-                  ("y0", c.cfg.y0), ("keep_solution", c.cfg.keep_solution))
+                  ("y0", c.cfg.y0), ("keep_solution", c.cfg.keep_solution),
+                  ("refinement", _native.current_refinement()))  # baked into the kernel's arguments
         return tuple((n, t.data_ptr()) for n, t in src) + consts
 
     def __call__(self) -> Tuple[torch.Tensor, torch.Tensor]:

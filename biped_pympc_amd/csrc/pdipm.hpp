@@ -49,8 +49,14 @@ struct SolverArgs {
   int scratch_slots;
   int scratch_stride;  // doubles per slot: the largest SolverLayout(N).total over N = 1..kMaxN
   int* status;  // (batch) per-problem status word (kStatus* bits), or null: not written
-  int refine_all;  // 1: the register kernels refine the affine direction in every iteration (srbd_set_refinement)
+  int refine_policy;  // the register kernels' refinement policy word (srbd_set_refinement_policy)
+  double refine_w;    // its W = z / s vote threshold (INFINITY: no W vote)
 };
+
+// Refinement policy word of the register kernels (include/srbd_mpc.h SRBD_REFINE_*): bit 0 the affine
+// direction in every iteration, bits 8-15 / 16-23 in the first / last k iterations, bits 24-25 the
+// combined direction's refinement (0 every iteration, 1 never, 2 the last ceil(K / 2), 3 dual rows only)
+constexpr int kRefineAffineAll = 1;
 
 // Per-problem status word (SURVEY.md 5 "failure detection"; the reference has only its clamps,
 // sparse_pdipm_solver.py:466-467,501-515): bit 0 a non-finite value in the returned x, s, z, y or
@@ -176,7 +182,9 @@ __device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
 // solve must keep the stiff direction: Phi_f reaches cond ~1e12 as the barrier sharpens, and an
 // explicit inverse applied to a vector loses the component along G_i (error ~cond x that of a stable
 // solve) that Lambda ~ W then multiplies into dz (scripts/stiff_dz_emu.py).
-template <int n>
+// kRcp: pivot reciprocals by rcp3 (~2^-46 relative; the register kernels' hot loop) instead of IEEE
+// division (the general and LDS-resident kernels, the accuracy baseline).
+template <int n, bool kRcp = false>
 __device__ inline void ldlt_factor(double (&a)[n * (n + 1) / 2]) {
   double d[n];
 #pragma unroll
@@ -185,7 +193,7 @@ __device__ inline void ldlt_factor(double (&a)[n * (n + 1) / 2]) {
 #pragma unroll
     for (int k = 0; k < j; ++k) dj -= a[j * (j + 1) / 2 + k] * a[j * (j + 1) / 2 + k] * d[k];
     d[j] = dj;
-    const double id = rcp3(dj);
+    const double id = kRcp ? rcp3(dj) : 1.0 / dj;
 #pragma unroll
     for (int i = j + 1; i < n; ++i) {
       double v = a[i * (i + 1) / 2 + j];

@@ -29,15 +29,6 @@
 #ifndef SRBD_SWP_INV
 #define SRBD_SWP_INV 0  // two-wave QPs invert their chain blocks by the software-pipelined sweep: measured slower, off
 #endif
-#ifndef SRBD_REFINE_AFFINE_ALL
-#define SRBD_REFINE_AFFINE_ALL 0  // refine the affine direction in every iteration (+18 % time; diagnostics)
-#endif
-#ifndef SRBD_AFFINE_REFINE_W
-#define SRBD_AFFINE_REFINE_W 1e3  // refine the affine direction when some row has z / s at least this
-#endif
-#ifndef SRBD_PIPE_FACTOR
-#define SRBD_PIPE_FACTOR 0  // stage-pipelined factorisation of two-wave QPs: built and measured slower, off
-#endif
 
 namespace srbd {
 
@@ -93,13 +84,7 @@ struct RegLayout {
                        end0 = DMY + 2,
                        // the fused prologue's FormerLds scratch from TV on (pads the short horizons)
                        former = TV + 2 * (int)((sizeof(FormerLds) + 15) / 16);
-  // The stage-pipelined factorisation of a two-wave QP (RegCtx::pipe_factor) keeps every stage's two
-  // inverted foot blocks Phi_f^-1 in PH (20 N doubles; the one-wave kernels use TV, dead at that
-  // point, as their scratch), where the QP still fits 4 per CU (160 KiB / 4): N <= 20.
-  static constexpr bool pipe = SRBD_PIPE_FACTOR && TPB == 128 &&
-                               8 * ((end0 + 20 * N) > former ? (end0 + 20 * N) : former) <= 40960;
-  static constexpr int PH = end0, end = end0 + (pipe ? 20 * N : 0), total = end > former ? end : former;
-  static_assert((PH & 1) == 0, "16-byte aligned foot blocks (read as double2)");
+  static constexpr int end = end0, total = end > former ? end : former;
   // SE: the three equality-row register slots of RegCtx::erow (dynamics rows {0,1,2,6,7,8} and
   // {3,4,5,9,10,11} of every stage, then the x-moment rows), whatever the horizon
   static constexpr int SI = (m + TPB - 1) / TPB, SE = 3, SX = (nx + TPB - 1) / TPB;
@@ -147,14 +132,6 @@ static __constant__ uint8_t c_dvslot[78] = {77, 58, 32, 73, 46, 5,  52, 54, 50, 
                                             37, 40, 67, 27, 26, 68, 60, 66, 57, 36, 59, 1,  45, 74, 56, 0,
                                             63, 7,  11, 12, 72, 10, 35, 25, 4,  16, 34, 62, 38, 13};
 
-// The pipelined S_ii build's entry of each lane (RegCtx::pipe_factor): pass A, lanes 0..63: the 21
-// dense x dense entries (positions 0..20 of the class-sorted table c_tab.dvo), then the 43 sparse-index
-// entries of foot position 0 or 1 and the first 7 of position 2; pass B, lanes 0..13: the other 14
-// entries of position 2 (tests/test_layout.py checks the partition)
-constexpr uint8_t kPipeEntry[78] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
-                                    16, 17, 18, 19, 20, 21, 22, 23, 26, 29, 30, 32, 33, 35, 36, 37, 39, 42, 43, 44, 45, 47, 49, 50, 54, 55, 56, 57, 58, 59, 60, 63, 64, 67, 70, 71, 72, 73, 74, 76, 77, 24, 25, 27, 28, 31, 34, 38, 40, 41, 46, 48, 51, 52, 53, 61, 62, 65, 66, 68, 69, 75};
-static __constant__ uint8_t c_pipe_entry[78] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
-                                                16, 17, 18, 19, 20, 21, 22, 23, 26, 29, 30, 32, 33, 35, 36, 37, 39, 42, 43, 44, 45, 47, 49, 50, 54, 55, 56, 57, 58, 59, 60, 63, 64, 67, 70, 71, 72, 73, 74, 76, 77, 24, 25, 27, 28, 31, 34, 38, 40, 41, 46, 48, 51, 52, 53, 61, 62, 65, 66, 68, 69, 75};
 
 // Byte offset, inside a step's block pair, of element (row r, column c) of chain lane l (group
 // g = l >> 4, row r = min(l & 15, 11), both in the group's coordinates): packed-lower slot of
@@ -431,16 +408,10 @@ struct RegCtx {
     }
   }
   static constexpr int mid = N / 2, nf = mid, nb = N - 1 - mid, T = nf > nb ? nf : nb;
-  // Stage-pipelined factorisation (two-wave QPs, RegLayout::pipe): wave 1 forms the stage blocks and
-  // the dual right-hand side in the order the chain consumes them while wave 0 runs the chain, and
-  // the per-stage tasks (foot blocks of Phi_u, the scalar u columns) live on wave 1's lanes: FB is
-  // their first lane (task fl = lane - FB)
-  static constexpr bool kPipe = Lo::pipe;
   // the chain's 12x12 block inverses by the software-pipelined sweep (inverse_rows12<true>), tried for
   // two-wave QPs on the premise that their chain wave runs alone on its SIMD (profiles/r05/simd_probe.txt:
   // its SIMD partner is another QP's second wave); measured +2.1 % at N = 20 (n20_pipeline.txt): off
   static constexpr bool kSwpInv = SRBD_SWP_INV && TPB == 128;
-  static constexpr int FB = kPipe ? 64 : 0;
   static constexpr int kFactorUnroll = T + 1;  // chains fully unrolled (N = 20: -4.7 % vs rolled)
   double* L;
   int lane;
@@ -453,17 +424,6 @@ struct RegCtx {
   static constexpr bool kArgRows = N == 21;
   int env_ = 0;
   const double *fp_ = nullptr, *hp_ = nullptr, *bp_ = nullptr;
-  // the pipelined S_ii build's two entries of this lane (pipe_factor), looked up once per solve:
-  // rows / columns of the pass-A and pass-B entries and their DV slots, 4 + 4 + 4 + 4 + 7 + 7 bits
-  int pipe_ix = 0;
-  __device__ void pipe_prep() {
-    const int lw = lane & 63;
-    const int ka = c_pipe_entry[lw], kb = c_pipe_entry[64 + (lw < 14 ? lw : 0)];
-    const int rca = c_tab.dvo[ka], rcb = c_tab.dvo[kb];
-    const int ra = rca & 15, ca = rca >> 4, rb = rcb & 15, cb = rcb >> 4;
-    const int sla = c_dvslot[ra * (ra + 1) / 2 + ca], slb = c_dvslot[rb * (rb + 1) / 2 + cb];
-    pipe_ix = ra | (ca << 4) | (rb << 8) | (cb << 12) | (sla << 16) | (slb << 23) | ((ka < 21) << 30);
-  }
   __device__ const double* fg() const { return kArgRows ? solver_in(kernel_args(), 3) + (size_t)env_ * nz : fp_; }
   __device__ const double* hg() const { return kArgRows ? solver_in(kernel_args(), 4) + (size_t)env_ * m : hp_; }
   __device__ const double* bg() const { return kArgRows ? solver_in(kernel_args(), 5) + (size_t)env_ * p : bp_; }
@@ -487,14 +447,8 @@ struct RegCtx {
   }
   // h of slot t (the CCS kernel re-reads its last slot from memory, see kFReg)
   __device__ double hval(int t, int q) const { return (kFReg || t < SI - 1) ? hvr[t] : hg()[q]; }
-  // ph: this foot-task lane's inverted foot block; the pipelined kernels re-read it from PH instead
-  // (20 VGPRs held across the Newton loop by every lane of both waves would spill the N = 20 kernel)
-  double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[kPipe ? 1 : 10];
-  // element e of foot task fl's inverted block (packed lower, sym_idx order)
-  __device__ void load_ph(int fl, double (&p)[10]) const {
-#pragma unroll
-    for (int e = 0; e < 10; ++e) p[e] = kPipe ? at(Lo::PH)[20 * (fl >> 1) + 10 * (fl & 1) + e] : ph[kPipe ? 0 : e];
-  }
+  // ph: this foot-task lane's LDL^T factors of its foot block Phi_f (foot_inverse, phi_solve)
+  double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
   double e3r[SI];  // the affine refinement's row-3 residuals (degenerate iterations only)
   PROF_DECL
 
@@ -684,7 +638,7 @@ struct RegCtx {
     // LDL^T factors for the solves (ph: phi_solve) and, from them, the inverse for the S_ii build (dst):
     // the Schur complement and the solves take the same Phi_f^-1 (a mismatched pair -- the sweep
     // inverse in S_ii, stable solves in dx -- left z 1e-4 off at K = 20)
-    ldlt_factor<4>(a);
+    ldlt_factor<4, true>(a);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       double ec[4] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0, c == 3 ? 1.0 : 0.0}, pc[4];
@@ -692,29 +646,15 @@ struct RegCtx {
 #pragma unroll
       for (int r = c; r < 4; ++r) dst[20 * i + 10 * f + r * (r + 1) / 2 + c] = pc[r];
     }
-    if constexpr (!kPipe) {
 #pragma unroll
-      for (int e = 0; e < 10; ++e) ph[e] = a[e];
-    }
+    for (int e = 0; e < 10; ++e) ph[e] = a[e];
   }
   // x = Phi_f^-1 v for foot task fl, by a stable solve with the lane's LDL^T factors: the explicit
   // inverse applied to v loses the stiff direction G_i dx of rows with W = z / s ~ 1e7..1e8, whose error
-  // Lambda ~ W multiplies into dz. The pipelined variant (kPipe, off) multiplies by the
-  // inverse it keeps in LDS.
+  // Lambda ~ W multiplies into dz.
   __device__ void phi_solve(int fl, const double (&v)[4], double (&x)[4]) const {
-    if constexpr (kPipe) {
-      double P[10];
-      load_ph(fl, P);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t += P[sym_idx(a, q)] * v[q];
-        x[a] = t;
-      }
-    } else {
-      ldlt_solve<4>(ph, v, x);
-    }
+    (void)fl;
+    ldlt_solve<4>(ph, v, x);
   }
 
   // Phi_u foot inverses and the S_ii blocks (parallel over the wave)
@@ -733,7 +673,7 @@ struct RegCtx {
       }
     }
     qp_sync<TPB>();
-    if (lane < 2 * N) foot_inverse(lane, PHs);  // (FB = 0 here)
+    if (lane < 2 * N) foot_inverse(lane, PHs);
     qp_sync<TPB>();
     // S_ii = K + sum_f N_f Phi_f^-1 N_f^T in two divergence-free passes over the class-sorted entry
     // table (TRI = c_tab.dvo: 21 dense x dense entries, then 57 with a sparse index): an entry
@@ -815,10 +755,8 @@ struct RegCtx {
 
   // kFwd: also the affine solve's forward elimination w_i = D_i^-1 (g_i - C w_{i-1}) with each
   // block's inverse row still in registers (g from solve_rhs(0) in QV; w_i written back over g_i)
-  // kWait (stage-pipelined factorisation): step t first waits until wave 1 has published the stages
-  // it reads (pipe_need(t) of them, flag values tag + count)
-  template <bool kFwd, bool kWait = false>
-  SRBD_PHASE_ATTR __device__ void factor_chain(int tag = 0) {
+  template <bool kFwd>
+  SRBD_PHASE_ATTR __device__ void factor_chain() {
     const int lane = fresh_lane();
     double* DV = at(Lo::DV);
     double* QV = at(Lo::QV);
@@ -858,7 +796,6 @@ struct RegCtx {
 #pragma unroll
         for (int c = 0; c < 12; ++c) X[c] = 0.0;
         const int imm = mstep ? kDvBytes * (N - 1) : 2 * kDvBytes * t;  // this step's blocks
-        if constexpr (kWait) pipe_wait(tag + pipe_need(t), t == 0);
         if (act) {
           if (!(mstep && g == 1)) {
 #pragma unroll
@@ -919,188 +856,6 @@ struct RegCtx {
     PROF_ADD(2);
   }
 
-  // ---------------------------------------------- stage-pipelined factorisation ----
-  // Two-wave QPs (kPipe): the block chain runs on wave 0 while wave 1 forms the stage blocks S_ii
-  // (DV), stage by stage in the order the chain consumes them, and publishes them through a flag word
-  // in LDS; the chain waits on it per step (s_sleep), not on a workgroup barrier. In the barrier-phased
-  // order (factor_build, solve_rhs<0>, factor_chain<true>) wave 1 idled through the whole chain
-  // (SQ_WAIT_ANY 55 % of an N = 20 wave's cycles, profiles/r04/sq_counters_fused_N20*). Same
-  // arithmetic in the same order per value (the sparse entries add their structural-zero slots as
-  // exact zeros). Built and measured 0.9-10 % SLOWER than the barrier-phased order (five variants,
-  // profiles/r05/n20_pipeline.txt): the chain waits for wave 1's per-iteration set-up and first stage
-  // pair, which is about what the barrier phase cost; off by default (SRBD_PIPE_FACTOR).
-  // k-th stage wave 1 produces: the pairs (t, N - 1 - t) of the steps both groups run, then group 0's
-  // remaining steps, the middle stage last
-  __device__ static int pipe_stage(int k) {
-    if (k == N - 1) return mid;
-    if (k < 2 * nb) return (k & 1) ? N - 1 - (k >> 1) : (k >> 1);
-    return nb + (k - 2 * nb);
-  }
-  // stages published before chain step t may start (the middle step, t = T: all of them)
-  __device__ static constexpr int pipe_need(int t) {
-    return t == T ? N : ((t + 1 < nf ? t + 1 : nf) + (t + 1 < nb ? t + 1 : nb));
-  }
-  __device__ int* pipe_flag() const { return reinterpret_cast<int*>(at(Lo::SG) + 14); }  // SG[14] unused
-  __device__ void pipe_wait(int want, bool first = false) {
-    const volatile int* f = pipe_flag();
-    const unsigned long long t0 = PROF_NOW();
-    (void)t0;
-    (void)first;
-    while (*f < want) __builtin_amdgcn_s_sleep(1);
-    PROF_SPAN(7, t0);  // diagnostic builds: cycles the chain waited for wave 1
-    if (first) PROF_SPAN(8, t0);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  }
-  // factor_build + solve_rhs<0> + factor_chain<true> of a two-wave QP; tag: flag base of this
-  // iteration (64 it: a published count never reaches the next iteration's base)
-  SRBD_PHASE_ATTR __device__ void pipe_factor(int tag) {
-    const int lane = fresh_lane();
-    double *VV = at(Lo::VV), *DV = at(Lo::DV), *TV = at(Lo::TV), *QV = at(Lo::QV), *Zr2 = at(Lo::Z),
-           *PH = at(Lo::PH);
-    const double *IX = at(Lo::IX), *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *K0 = at(Lo::K0),
-                 *K1 = at(Lo::K1);
-#pragma unroll
-    for (int t = 0; t < SI; ++t) {  // W, D^-1, Lambda (factor_build's rows)
-      const int q = lane + TPB * t;
-      if (RegCtx<N>::full_slot(t, m) || q < m) {
-        wd[t] = rcp3(s[t]) * z[t] + kDelta;
-        di[t] = rcp3(1.0 + kDelta * wd[t]);
-        VV[q] = di[t] * wd[t];
-      }
-    }
-    qp_sync<TPB>();
-    const int fl = lane - FB;
-    if ((unsigned)fl < 2u * N) foot_inverse(fl, PH);  // wave 1's lanes: the per-stage tasks live there
-    qp_sync<TPB>();
-#pragma unroll
-    for (int t = 0; t < SI; ++t) {  // solve_rhs<0>'s rows: r2 (parked in Z), VV = D^-1 (r2 + W r_s)
-      const int q = lane + TPB * t;
-      if (RegCtx<N>::full_slot(t, m) || q < m) {
-        const double si = rcp3(s[t]);
-        const double r2 = -(si * (s[t] * z[t]));
-        Zr2[q] = r2;
-        VV[q] = di[t] * (r2 + wd[t] * rs[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < SX; ++t) {  // the x columns of t
-      const int c = lane + TPB * t;
-      if (full_slot(t, nx) || c < nx) TV[c] = -rxx[t] * IX[c - m24(div12(c), 12)];
-    }
-    qp_sync<TPB>();
-    rhs_tasks<0>(fl, false);  // t on the foot and scalar u columns
-    qp_sync<TPB>();
-    g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
-    g_slot<1>(TV, Mc, Pd, Nd, QV);
-    qp_sync<TPB>();
-    if (__builtin_amdgcn_readfirstlane(lane) >= 64) {  // ---- wave 1: producer (wave-uniform branch) ----
-      const unsigned long long tsplit = PROF_NOW();
-      (void)tsplit;
-      const int lw = lane & 63;
-      double W[20], WB[8];
-      int slA, slB;
-      double kA0, kA1, kB0, kB1;
-      {
-        const int ix = pipe_ix;
-        const int ra = ix & 15, ca = (ix >> 4) & 15, rb = (ix >> 8) & 15, cb = (ix >> 12) & 15;
-        const int sya = ra * (ra + 1) / 2 + ca, syb = rb * (rb + 1) / 2 + cb;
-        slA = (ix >> 16) & 127;
-        slB = (ix >> 23) & 127;
-        kA0 = K0[sya];
-        kA1 = K1[sya];
-        if (ix >> 30) {  // dense x dense (factor_build's w)
-#pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            double vr[4], vc[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-              vr[a] = Nd[nd_idx(ra, foot_colj(f, a))];
-              vc[a] = Nd[nd_idx(ca, foot_colj(f, a))];
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-              for (int b = 0; b <= a; ++b)
-                W[10 * f + a * (a + 1) / 2 + b] = a == b ? vr[a] * vc[a] : vr[a] * vc[b] + vr[b] * vc[a];
-          }
-        } else {  // sparse index (factor_build's wn at slots sym_idx(as, b))
-          const bool rsp = (ra % 6) >= 3;
-          const int sp = rsp ? ra : ca, dn = rsp ? ca : ra, as = sp % 3;
-#pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            const double ns = Nd[nd_idx(sp, foot_colj(f, as))];
-            double wn[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) wn[b] = ns * Nd[nd_idx(dn, foot_colj(f, b))];
-#pragma unroll
-            for (int e = 0; e < 10; ++e) {  // slot e = sym_idx(as, b) holds wn[b], the others 0
-              double v = 0.0;
-#pragma unroll
-              for (int b = 0; b < 4; ++b) v = (sym_idx_c(as, b) == e) ? wn[b] : v;
-              W[10 * f + e] = v;
-            }
-          }
-        }
-        kB0 = K0[syb];
-        kB1 = K1[syb];
-        const bool rspb = (rb % 6) >= 3;
-        const int spb = rspb ? rb : cb, dnb = rspb ? cb : rb;  // foot position spb % 3 = 2
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const double ns = Nd[nd_idx(spb, foot_colj(f, 2))];
-#pragma unroll
-          for (int b = 0; b < 4; ++b) WB[4 * f + b] = ns * Nd[nd_idx(dnb, foot_colj(f, b))];
-        }
-    
-      }
-      // Each lane of wave 1 holds the weights of S_ii entries for the whole pass: pass A, every lane,
-      // entry c_pipe_entry[lw] with its stage-invariant products expanded to the 20 packed Phi^-1 slots
-      // (a dense x dense entry: the 10 pair products per foot of factor_build; a sparse-index entry: its
-      // 4 products per foot at slots sym_idx(as, b), zeros elsewhere -- the nonzero terms then add in
-      // factor_build's order); pass B, lanes < 14, one more sparse entry of foot position as = 2 (the
-      // 21 dense + 57 sparse entries = 64 + 14; 14 of the 21 as = 2 entries go to pass B)
-      PROF_SPAN(10, tsplit);
-      // stage i's block: both passes from the stage's 20 Phi^-1 values (16-byte broadcast reads)
-      auto sii_stage = [&](int i) {
-        double P[20];
-        const double2* p2 = reinterpret_cast<const double2*>(PH + 20 * i);
-#pragma unroll
-        for (int e = 0; e < 10; ++e) {
-          const double2 v2 = p2[e];
-          P[2 * e] = v2.x;
-          P[2 * e + 1] = v2.y;
-        }
-        double va = i == 0 ? kA0 : kA1;
-#pragma unroll
-        for (int e = 0; e < 20; ++e) va += P[e] * W[e];
-        DV[kDvStride * dv_pos<N>(i) + slA] = va;
-        if (lw < 14) {
-          double vb = i == 0 ? kB0 : kB1;
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) vb += P[10 * f + sym_idx_c(2, b)] * WB[4 * f + b];
-          DV[kDvStride * dv_pos<N>(i) + slB] = vb;
-        }
-      };
-      // the chain's first step (stages 0 and N - 1) from both waves before it starts, one stage each
-#pragma unroll 1
-      for (int k = 0; k < N; ++k) {
-        sii_stage(pipe_stage(k));
-        if (k >= 2 * nb || (k & 1)) {  // publish the step's stages
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lw == 0) *(volatile int*)pipe_flag() = tag + k + 1;
-          if (k == 1) PROF_SPAN(9, tsplit);
-        }
-      }
-      PROF_ADD(2);  // diagnostic builds: wave 1's production time (slot 8 + 2)
-    } else {  // ---- wave 0: the chain, step by step as its stages are published ----
-      factor_chain<true, true>(tag);  // (ends in the workgroup barrier both waves meet below)
-      return;
-    }
-    qp_sync<TPB>();
-  }
-
   // ------------------------------------------------------------------------ solve ----
   // kMode 0: affine rhs r2 = -(S^-1 (s o z)); 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu).
   // One solve = solve_rhs (t = Phi^-1 r~ and the dual right-hand side g, in QV) -> solve_chain
@@ -1108,10 +863,10 @@ struct RegCtx {
   // dz, ds). The affine solve's forward elimination runs inside factor_chain<true> instead, with
   // each block's inverse still in registers (solve_chain<true> then only substitutes back).
   template <int kMode>
-  __device__ void solve(double smu, bool rx = false) {
+  __device__ void solve(double smu, bool rx = false, bool step0 = true) {
     solve_rhs<kMode>(smu, rx);
     solve_chain<false>();
-    solve_finish<false, false, true>();
+    solve_finish<false, false, true>(step0);
   }
 
   // One step of iterative refinement of the combined direction d = (dx, ds, dz, dy) against the
@@ -1153,8 +908,9 @@ struct RegCtx {
   // kAff: the affine (predictor) direction at a degenerate iterate (see the main loop): r_s stays
   // (the combined solve needs it), e3 goes to Z for solve_finish<true, true>, and dy is not parked
   // (RXu still feeds the combined solve)
+  // row1 = false (refinement policy 3): the dual rows only -- no KKT row-1 foot correction
   template <bool kAff = false>
-  SRBD_PHASE_ATTR __device__ void refine_rhs() {
+  SRBD_PHASE_ATTR __device__ void refine_rhs(bool row1 = true) {
     const int lane = fresh_lane();
     const double *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
     double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z);
@@ -1177,8 +933,8 @@ struct RegCtx {
       }
     }
     qp_sync<TPB>();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
-    const int fl = lane - FB;
-    if ((unsigned)fl < 2u * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
+    const int fl = lane;
+    if (row1 && (unsigned)fl < 2u * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
       const int i = fl >> 1, f = fl & 1, b = 12 * i;
       const double* zf = Zd + 16 * i + 8 * f;
       const double* RXu = DYs;
@@ -1250,7 +1006,7 @@ struct RegCtx {
       if ((kMode == 0 || rx) && (full_slot(t, nx) || c < nx)) TV[c] = -rxx[t] * IX[c - m24(div12(c), 12)];
     }
     qp_sync<TPB>();
-    rhs_tasks<kMode>(lane - FB, rx);
+    rhs_tasks<kMode>(lane, rx);
     qp_sync<TPB>();
     g_slot<0>(TV, Mc, Pd, Nd, QV);  // g = A_dyn t + r_e (dynamics rows, owner of r_e)
     g_slot<1>(TV, Mc, Pd, Nd, QV);
@@ -1258,7 +1014,7 @@ struct RegCtx {
     PROF_ADD(3);
   }
 
-  // solve_rhs's per-stage tasks fl = lane - FB: t = Phi^-1 r1~ on the foot columns (fl < 2 N),
+  // solve_rhs's per-stage tasks fl = lane: t = Phi^-1 r1~ on the foot columns (fl < 2 N),
   // r1~ = -r_x - G^T VV (G only on the foot columns, each foot through its 8 rows), and the scalar u
   // columns of t (2 N <= fl < 3 N, affine solve or rx only)
   template <int kMode>
@@ -1395,9 +1151,10 @@ struct RegCtx {
   // columns, so dx is finished on those alone (no x columns, no scalar columns, no x-moment duals).
   // kStep0: refine_rhs's step 0 for the combined direction fused into the row loop, where dz, ds,
   // G dx and VV are at hand -- e2, e3, q = D^-1 (e2 - W e3); VV += q, Z = dz + q for G^T (dz + q),
-  // r_s -= e3
+  // r_s -= e3 (step0 false: skipped at run time -- an iteration whose combined direction the refinement
+  // policy leaves unrefined or refines in the dual rows only)
   template <bool kRefine = false, bool kAffine = false, bool kStep0 = false>
-  SRBD_PHASE_ATTR __device__ void solve_finish() {
+  SRBD_PHASE_ATTR __device__ void solve_finish(bool step0 = true) {
     const int lane = fresh_lane();
     double *VV = at(Lo::VV), *TV = at(Lo::TV), *QV = at(Lo::QV), *DYm = at(Lo::DYm);
     const double *RXu = at(Lo::RXu), *REm = at(Lo::REm), *IX = at(Lo::IX), *Gf = at(Lo::Gf),
@@ -1413,7 +1170,7 @@ struct RegCtx {
         TV[c] = TV[c] - aty * IX[j];
       }
     }
-    const int fl = lane - FB;
+    const int fl = lane;
     if ((unsigned)fl < (unsigned)((kAffine ? 2 : 3) * N)) {
       const bool foot = kAffine || fl < 2 * N;
       const int i = foot ? (fl >> 1) : fl - 2 * N;
@@ -1461,7 +1218,7 @@ struct RegCtx {
         // the affine refinement keeps r_s and parks its row-3 residual e3 in Z (refine_rhs<true>)
         const double r3 = (kRefine && kAffine) ? at(Lo::Z)[q] - rs[t] : -rs[t];
         ds[t] = r3 - gd + kDelta * dz[t];
-        if constexpr (kStep0) {
+        if (kStep0 && step0) {
           double* Zd = at(Lo::Z);
           const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
           const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
@@ -1538,7 +1295,8 @@ struct FusedArgs {
   float* tau;      // (B, 2, ndof) float32, or null
   int ndof;
   int* status;     // (B) per-problem status word (pdipm.hpp kStatus*), or null
-  int refine_all;  // 1: refine the affine direction in every iteration (srbd_set_refinement)
+  int refine_policy;  // srbd_set_refinement_policy's word (include/srbd_mpc.h SRBD_REFINE_*)
+  double refine_w;    // the W = z / s vote's threshold (INFINITY: no W vote)
 };
 
 // Body shared by the solver kernel (kFused = false: the QP comes from qp_former's CCS outputs and is
@@ -1755,7 +1513,6 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     SG[7] = e9;
     SG[8] = 1.0 / (p6 * kDelta + e6 * e6);
     SG[9] = 1.0 / (p9 * kDelta + e9 * e9);
-    *reinterpret_cast<int*>(SG + 14) = 0;  // RegCtx::pipe_flag: nothing published yet
   }
   qp_sync<TPB>();
   if (lane < 24) {  // compact M and C (C = M diag(P / phi_x)); group 1's block is pi C^T pi^T
@@ -1841,9 +1598,10 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
   const double* QV = smem + Lo::QV;
   const double* DYm = smem + Lo::DYm;
   const double* RXu = smem + Lo::RXu;
-  if constexpr (RegCtx<N, kFused>::kPipe) C.pipe_prep();
   PROF_MARK_CTX(C);
   const int n_iter = kFused ? fa.n_iter : args.n_iter;
+  const int rpol = kFused ? fa.refine_policy : args.refine_policy;
+  const double rw = kFused ? fa.refine_w : args.refine_w;
   for (int it = 0; it < n_iter; ++it) {
     if constexpr (TPB == 64 && SRBD_PROGRESS_PRIO) {
       // Wave priority falls with this QP's progress (3 over the first quarter of the iterations, 0
@@ -1858,14 +1616,15 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
-    // An ill-conditioned iterate -- some row with W = z / s >= SRBD_AFFINE_REFINE_W (1e3), e.g. an s
+    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (1e3 by default), e.g. an s
     // at or near its 1e-8 clamp (sparse_pdipm_solver.py:520) -- is where the reduced solve's affine
     // ds, dz lose digits; their error enters sigma and the corrector, and the trajectory drifts from the
     // reference's (profiles/r02/refinement_4row.txt; round 5: scripts/parity_fuzz.py found iterates at
     // W 4.5e3 .. 1.2e8 with s above the clamp drifting to 1e-4 in z, profiles/r05/parity_fuzz.txt).
     // Such iterations also refine the affine direction (the QP is one wave or joined ones: a uniform
-    // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations. srbd_set_refinement(1)
-    // refines it in every iteration, as the LDS-resident and general kernels always do.
+    // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations. The refinement policy
+    // (srbd_set_refinement_policy, a kernel argument) adds iterations by position: every one
+    // (srbd_set_refinement(1), as the LDS-resident and general kernels always do), the first k, the last k.
     bool degen;
     {
       const int l = C.fresh_lane();
@@ -1873,9 +1632,14 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
 #pragma unroll
       for (int t = 0; t < SI; ++t)
         if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m)
-          p = p || (C.s[t] <= 1e-8) || (C.z[t] >= SRBD_AFFINE_REFINE_W * C.s[t]);
-      degen = SRBD_REFINE_AFFINE_ALL || (kFused ? fa.refine_all : args.refine_all) || C.block_any(p);
+          p = p || (C.s[t] <= 1e-8) || (C.z[t] >= rw * C.s[t]);
+      degen = (rpol & kRefineAffineAll) || it < ((rpol >> 8) & 255) || it >= n_iter - ((rpol >> 16) & 255) ||
+              C.block_any(p);
     }
+    // the combined direction's refinement (policy bits 24-25): every iteration (default), never, the
+    // last ceil(K / 2) iterations, or the dual rows (KKT row 4) only
+    const int cpol = (rpol >> 24) & 3;
+    const bool refc = cpol == 0 || cpol == 3 || (cpol == 2 && it >= n_iter / 2);
     int ul = C.fresh_lane();
     if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)
       double a = 0.0, b = 0.0, c = 0.0;
@@ -1893,13 +1657,9 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
       res2 = sqrt(C.block_sum(c));
     }
     PROF_ADD_CTX(C, 0);
-    if constexpr (RegCtx<N, kFused>::kPipe) {
-      C.pipe_factor(64 * it);  // the same three phases, wave 1 feeding wave 0's chain stage by stage
-    } else {
-      C.factor_build();
-      C.template solve_rhs<0>(0.0);
-      C.template factor_chain<true>();  // + the affine forward elimination
-    }
+    C.factor_build();
+    C.template solve_rhs<0>(0.0);
+    C.template factor_chain<true>();  // + the affine forward elimination
     C.template solve_chain<true>();
     if (degen) {  // full affine finish (rho needs all of dx), then the 4-row refinement
       C.template solve_finish<false, false>();
@@ -1921,13 +1681,17 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     const double sigma = ratio * ratio * ratio;  // (mu_aff / mu)^3, sparse_pdipm_solver.py:487
     qp_sync<TPB>();
     PROF_ADD_CTX(C, 5);
-    C.template solve<1>(sigma * mu * 1.0, degen);  // (spelling the phases out here costs N = 20 spills)
-    // one refinement step in EVERY iteration: refining only the last 1 or 3 iterations leaves the
-    // K = 10 / 20 parity where no refinement has it, only the first 3 / 5 / 7 lets the degenerate
-    // duals of K = 20 drift to 2e-5 (profiles/r02/refinement_parity.txt, refinement_variants.txt)
-    C.refine_rhs();
-    C.template solve_chain<false>();
-    C.template solve_finish<true>();
+    // (spelling the phases out here costs N = 20 spills)
+    C.template solve<1>(sigma * mu * 1.0, degen, refc && cpol != 3);
+    // one refinement step in EVERY iteration by default: in round 2 (explicit foot-block inverses)
+    // refining only the last 1 or 3 iterations left the K = 10 / 20 parity where no refinement has it,
+    // only the first 3 / 5 / 7 let the degenerate duals of K = 20 drift to 2e-5
+    // (profiles/r02/refinement_parity.txt, refinement_variants.txt); round 6 re-measures
+    if (refc) {
+      C.refine_rhs(cpol != 3);
+      C.template solve_chain<false>();
+      C.template solve_finish<true>();
+    }
     double apc, adc;
     C.step_lengths(apc, adc);
     // status bit 1 (a step length at its 1e-12 floor in the last iteration), kept in LDS: SG[15] is
@@ -1953,12 +1717,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
         szn += sn * zn;
       }
     }
-    // dy = the combined solve's dy (parked in RXu by refine_rhs) + the refinement's correction
+    // dy = the combined solve's dy (parked in RXu by refine_rhs) + the refinement's correction (an
+    // unrefined iteration: the combined solve's dy, in QV)
 #pragma unroll
     for (int t = 0; t < (p + TPB - 1) / TPB; ++t) {
       const int e = ul + TPB * t;
       if (RegCtx<N>::full_slot(t, p) || e < p) {
-        const double dye = e < nx ? RXu[e] + QV[e] : DYm[e - nx];
+        const double dye = e < nx ? (refc ? RXu[e] : 0.0) + QV[e] : DYm[e - nx];
         Y[e] = Y[e] + adc * dye;
       }
     }

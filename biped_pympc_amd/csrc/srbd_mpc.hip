@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -75,13 +76,30 @@ int solver_path() {
   return p ? *p : 0;
 }
 
-// Affine refinement per device (srbd_set_refinement): 0 = on ill-conditioned iterates (z / s >= 1e3 in
-// some row, or an s at its clamp), 1 = in every iteration. Read by the register kernels only (the
-// LDS-resident and general kernels refine the affine direction in every iteration).
-srbd::PerDevice<int> g_refinement;
+// Refinement policy per device (srbd_set_refinement / srbd_set_refinement_policy). Mode 0 (default):
+// the affine direction on ill-conditioned iterates (z / s >= 1e3 in some row, or an s at its clamp),
+// the combined one in every iteration; mode 1: both in every iteration; mode 2: a policy word set by
+// srbd_set_refinement_policy. Read by the register kernels only (the LDS-resident and general kernels
+// refine both directions in every iteration).
+struct RefinePolicy {
+  int mode = 0;
+  int flags = 0;
+  double w = 0.0;
+};
+constexpr double kDefaultRefineW = 1e3;
+srbd::PerDevice<RefinePolicy> g_refinement;
 int refinement_mode() {
-  const int* p = g_refinement.at(current_device());
-  return p ? *p : 0;
+  const RefinePolicy* p = g_refinement.at(current_device());
+  return p ? p->mode : 0;
+}
+// the kernel arguments of the policy in effect: the word and the W threshold
+template <class Args>
+void set_refinement_args(Args& a) {
+  const RefinePolicy* p = g_refinement.at(current_device());
+  const int mode = p ? p->mode : 0;
+  a.refine_policy = mode == 2 ? p->flags : (mode == 1 ? SRBD_REFINE_AFFINE_ALL : 0);
+  const double w = mode == 2 ? p->w : kDefaultRefineW;
+  a.refine_w = w > 0.0 ? w : INFINITY;
 }
 
 int ensure_lds_attr(const void* fn, size_t bytes, srbd::LdsAttr& cache) {
@@ -132,6 +150,11 @@ int general_slot_doubles() {
 srbd::PerDevice<ScratchPool> g_scratch;
 srbd::PerDevice<int> g_scratch_cap;  // srbd_set_scratch_slots per device; 0 = default
 std::mutex g_scratch_mu;
+// A solver launch holds g_pool_rw shared from attaching the pool to its arguments until the kernel is
+// enqueued; srbd_release_device / a resizing srbd_set_scratch_slots take it exclusively before their
+// hipDeviceSynchronize, so a pool is never freed between another thread's attach and its launch (the
+// kernel would run on freed HBM). Lock order: g_pool_rw, then g_scratch_mu.
+std::shared_mutex g_pool_rw;
 
 // slots of a new pool on device `dev` with `cus` compute units
 int pool_slots(int dev, int cus) {
@@ -211,8 +234,9 @@ int launch_solver(const srbd::SolverArgs& a0, hipStream_t s) {
   if (a0.batch == 0) return 0;
   static srbd::LdsAttr cfg_general, cfg_fast, cfg_fast10, cfg_fast20;
   srbd::SolverArgs a = a0;
-  a.refine_all = refinement_mode();
+  set_refinement_args(a);
   const int path = solver_path();
+  std::shared_lock<std::shared_mutex> keep_pool(g_pool_rw);  // until the launch is enqueued
   // the stage-invariant kernels solve any other QP of the batch in the same launch (scratch pool)
   if (path != 1)
     if (int rc = attach_scratch(a, s)) return rc;
@@ -318,9 +342,20 @@ int srbd_get_solver_path(void) { return solver_path(); }
 int srbd_set_refinement(int mode) {
   if (mode < 0 || mode > 1)
     return set_error(kErrInvalid, "srbd_set_refinement: 0 (ill-conditioned iterates) or 1 (every iteration)");
-  int* p = g_refinement.at(current_device());
+  RefinePolicy* p = g_refinement.at(current_device());
   if (!p) return set_error((int)hipErrorInvalidDevice, "srbd_set_refinement: no current HIP device");
-  *p = mode;
+  *p = RefinePolicy{mode, 0, 0.0};
+  return 0;
+}
+
+int srbd_set_refinement_policy(int flags, double w) {
+  const int known = SRBD_REFINE_AFFINE_ALL | SRBD_REFINE_AFFINE_FIRST(255) | SRBD_REFINE_AFFINE_LAST(255) |
+                    SRBD_REFINE_COMBINED(3);
+  if ((flags & ~known) != 0 || w != w)
+    return set_error(kErrInvalid, "srbd_set_refinement_policy: unknown policy bits or a NaN threshold");
+  RefinePolicy* p = g_refinement.at(current_device());
+  if (!p) return set_error((int)hipErrorInvalidDevice, "srbd_set_refinement_policy: no current HIP device");
+  *p = RefinePolicy{2, flags, w};
   return 0;
 }
 
@@ -332,6 +367,7 @@ int srbd_prepare_device(void) {
 }
 
 int srbd_release_device(void) {
+  std::unique_lock<std::shared_mutex> no_launch(g_pool_rw);
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   ScratchPool* pool = g_scratch.at(current_device());
   if (!pool) return set_error((int)hipErrorInvalidDevice, "srbd_release_device: no current HIP device");
@@ -340,6 +376,7 @@ int srbd_release_device(void) {
 
 int srbd_set_scratch_slots(int slots) {
   if (slots < 0) return set_error(kErrInvalid, "srbd_set_scratch_slots: slots >= 0 (0 = one per resident workgroup)");
+  std::unique_lock<std::shared_mutex> no_launch(g_pool_rw);
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   const int dev = current_device();
   int* cap = g_scratch_cap.at(dev);
@@ -501,7 +538,7 @@ int srbd_mpc_solve(int horizon, int n_iter, int batch, double y0, const double* 
 static int launch_step(const srbd::FusedArgs& a0, hipStream_t st) {
   static srbd::LdsAttr cfg_lds;
   srbd::FusedArgs a = a0;
-  a.refine_all = refinement_mode();
+  set_refinement_args(a);
   if (srbd::regn::supported(a.N)) {
     srbd::regn::launch_step(a.N, a, st);  // static LDS (RegLayout)
   } else if (a.N != 10 && a.N != 20) {

@@ -144,8 +144,23 @@ int srbd_get_solver_path(void);
  * all within 8x the FP64 floor, against 10 and 19 in mode 0.
  * Returns 0, or an error for another mode. */
 int srbd_set_refinement(int mode);
-/* The refinement mode in effect for the current HIP device (0 if never set). */
+/* The refinement mode in effect for the current HIP device (0 if never set; 2 after
+ * srbd_set_refinement_policy). */
 int srbd_get_refinement(void);
+
+/* Diagnostics (A/B campaigns, scripts/parity_fuzz.py): an explicit refinement policy for the register
+ * kernels on the current device, in place of the mode. flags: SRBD_REFINE_AFFINE_ALL (the affine
+ * direction in every iteration), SRBD_REFINE_AFFINE_FIRST(k) / SRBD_REFINE_AFFINE_LAST(k) (in the first /
+ * last k iterations), and one SRBD_REFINE_COMBINED(c) for the combined direction: 0 every iteration (the
+ * modes' choice), 1 never, 2 the last ceil(K / 2) iterations, 3 the dual rows (KKT row 4) only, every
+ * iteration. w: the affine vote's W = z / s threshold (mode 0 uses 1e3; w <= 0: no W vote; an s at its
+ * clamp always votes). srbd_set_refinement(mode) returns to a mode. Returns 0, or an error for unknown
+ * bits or a NaN w. */
+#define SRBD_REFINE_AFFINE_ALL 1
+#define SRBD_REFINE_AFFINE_FIRST(k) (((k) & 255) << 8)
+#define SRBD_REFINE_AFFINE_LAST(k) (((k) & 255) << 16)
+#define SRBD_REFINE_COMBINED(c) (((c) & 3) << 24)
+int srbd_set_refinement_policy(int flags, double w);
 
 /* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the
  * stage-invariant kernels (one slot per resident workgroup -- 2048 on an MI355X of

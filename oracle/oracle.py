@@ -91,10 +91,15 @@ def _status_arg(status):
     return None if status is None else status.ctypes.data_as(_I32P)
 
 
-def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0, status: np.ndarray | None = None):
+ORDERS = {"md": 0, "amd": 1}  # the KKT elimination order: exact minimum degree (the checker), CasADi's AMD
+
+
+def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0, status: np.ndarray | None = None,
+          order: str = "md"):
     """inputs: Q_val, G_val, A_val, f, h, b, x, s, z, y as (B, nnz). Returns x, s, z, y, res(4), mu(1).
     status: an int32 (B,) array receiving the per-problem status word (srbd_oracle.c); with it a
-    failed factorisation is reported there (STATUS_LDL_FAIL) instead of raising."""
+    failed factorisation is reported there (STATUS_LDL_FAIL) instead of raising. order: "md" (exact
+    minimum degree, the checker) or "amd" (approximate minimum degree, the order of CasADi's ldl)."""
     register(N)
     d = layout.Dims(N)
     single = np.asarray(inputs[0]).ndim == 1
@@ -102,8 +107,9 @@ def pdipm(N: int, n_iter: int, inputs, B: int | None = None, nthreads: int = 0, 
         B = 1 if single else np.asarray(inputs[0]).shape[0]
     ins = [_as_batch(a, w, B) for a, w in zip(inputs, d.solver_in_nnz)]
     outs = [np.zeros((B, w)) for w in d.solver_out_nnz]
-    rc = lib().oracle_pdipm_batch(ctypes.c_int(N), ctypes.c_int(n_iter), ctypes.c_int(B),
-                                  _ptr_array(ins), _ptr_array(outs), ctypes.c_int(nthreads), _status_arg(status))
+    rc = lib().oracle_pdipm_batch_ord(ctypes.c_int(N), ctypes.c_int(n_iter), ctypes.c_int(B), _ptr_array(ins),
+                                      _ptr_array(outs), ctypes.c_int(nthreads), _status_arg(status),
+                                      ctypes.c_int(ORDERS[order]))
     if rc < 0:
         raise RuntimeError("oracle_pdipm_batch failed")
     if rc > 0:
@@ -130,9 +136,30 @@ def mpc_solve(N: int, n_iter: int, former_inputs, y0: float = 1.0, B: int | None
     return outs
 
 
-def kkt_stats(N: int) -> dict:
+def kkt_stats(N: int, order: str = "md") -> dict:
     register(N)
     n, nk, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    if lib().oracle_kkt_stats(ctypes.c_int(N), ctypes.byref(n), ctypes.byref(nk), ctypes.byref(nl)):
+    if lib().oracle_kkt_stats_ord(ctypes.c_int(N), ctypes.c_int(ORDERS[order]), ctypes.byref(n), ctypes.byref(nk),
+                                  ctypes.byref(nl)):
         raise RuntimeError("oracle_kkt_stats failed")
     return {"n": n.value, "nnz_kkt": nk.value, "nnz_L": nl.value}
+
+
+def kkt_order(N: int, order: str = "md") -> np.ndarray:
+    """The KKT elimination order (perm[k] = the row eliminated k-th) under `order`."""
+    register(N)
+    n = kkt_stats(N, order)["n"]
+    perm = np.zeros(n, np.int32)
+    if lib().oracle_kkt_order(ctypes.c_int(N), ctypes.c_int(ORDERS[order]), _iptr(perm)) != n:
+        raise RuntimeError("oracle_kkt_order failed")
+    return perm
+
+
+def amd_order(n: int, Kp, Ki) -> np.ndarray:
+    """srbd_oracle.c amd_order (CasADi's ldl ordering, restated) of a symmetric CSC pattern."""
+    Kp = np.ascontiguousarray(Kp, np.int32)
+    Ki = np.ascontiguousarray(Ki, np.int32)
+    perm = np.zeros(n, np.int32)
+    if lib().oracle_amd_order(ctypes.c_int(n), _iptr(Kp), _iptr(Ki), _iptr(perm)):
+        raise RuntimeError("oracle_amd_order failed")
+    return perm

@@ -23,7 +23,9 @@ def _if_else_step(v, dv):
     return max(min(1.0, 0.99 * np.fmin.reduce(cand)), 1e-12)
 
 
-def pdipm_dense(N: int, n_iter: int, Hv, Gv, Av, f, h, b, x, s, z, y):
+def pdipm_dense(N: int, n_iter: int, Hv, Gv, Av, f, h, b, x, s, z, y, factor_once: bool = False):
+    """factor_once: one LU (scipy lu_factor) per iteration for both solves -- the same restatement at half
+    the cost, for the parity campaign's per-env floors (scripts/parity_floor.py)."""
     nz, m, p = 24 * N, 16 * N, 14 * N
     H = layout.to_dense(Hv, *layout.ccs_H(N), (nz, nz))
     G = layout.to_dense(Gv, *layout.ccs_G(N), (m, nz))
@@ -50,14 +52,20 @@ def pdipm_dense(N: int, n_iter: int, Hv, Gv, Av, f, h, b, x, s, z, y):
         K[nz + 2 * m:, :nz] = A
         K[nz + 2 * m:, nz + 2 * m:] = -DELTA * np.eye(p)
         rhs = np.concatenate([-rx, -(sinv * (s * z)), -rs, -re])
-        sa = np.linalg.solve(K, rhs)
+        if factor_once:
+            from scipy.linalg import lu_factor, lu_solve
+            lu = lu_factor(K, check_finite=False)
+            solve = lambda r: lu_solve(lu, r, check_finite=False)  # noqa: E731
+        else:
+            solve = lambda r: np.linalg.solve(K, r)  # noqa: E731
+        sa = solve(rhs)
         dsa, dza = sa[nz:nz + m], sa[nz + m:nz + 2 * m]
         ap, ad = _if_else_step(s, dsa), _if_else_step(z, dza)
         mu_aff = (s + ap * dsa) @ (z + ad * dza) / m
         sigma = (mu_aff / mu) ** 3
         rc = s * z + dsa * dza - sigma * mu
         rhs_c = np.concatenate([np.zeros(nz), -(sinv * rc), np.zeros(m), np.zeros(p)])
-        d = sa + np.linalg.solve(K, rhs_c)
+        d = sa + solve(rhs_c)
         dx, ds, dz, dy = d[:nz], d[nz:nz + m], d[nz + m:nz + 2 * m], d[nz + 2 * m:]
         apc, adc = _if_else_step(s, ds), _if_else_step(z, dz)
         x = x + apc * dx

@@ -18,7 +18,10 @@
  *   - jacobian(): forward-mode AD (dual numbers) through the literal RK4 of forward_dynamics.
  *   - b = A z - eq(z), d = G z - ineq(z), f = grad - H z evaluated at the caller's z (x, u inputs).
  *   - ca.ldl / ca.ldl_solve: sparse LDL^T without numeric pivoting after a fill-reducing symmetric
- *     ordering (CasADi uses AMD; this file uses exact minimum degree -> same maths, other rounding).
+ *     ordering. The checker's ordering is exact minimum degree; CasADi's ldl(A, amd=True) orders by
+ *     approximate minimum degree, restated below as a second ordering (amd_order: Amestoy, Davis & Duff
+ *     1996 in the form of CSparse's cs_amd, order 1) -- the same maths, the reference's rounding path as
+ *     far as the ordering goes (oracle_pdipm_batch_ord; tests/test_oracle.py compares the two).
  *   - if_else(c, a, b) = if_else_zero(c, a) + if_else_zero(!c, b); fmin/fmax are C99 (NaN-ignoring).
  */
 #include <math.h>
@@ -131,12 +134,17 @@ typedef struct {
   int nH, nA, nG;
   int *Hp, *Hi, *Ap, *Ai, *Gp, *Gi;
   /* symbolic LDL of the full KKT (built lazily) */
-  int ldl_ready;
+  int kkt_ready;
   int n, nnzK;
   int *Kp, *Ki;   /* CSC of the permuted-free full symmetric KKT pattern */
   int *Ksrc;      /* per KKT entry: source code (see kkt_fill) */
-  int *Perm, *Pinv, *Lp, *Parent;
+  struct {        /* per ordering (ORDER_MD exact minimum degree, ORDER_AMD approximate) */
+    int ready;
+    int *Perm, *Pinv, *Lp, *Parent;
+  } sym[2];
 } pattern_t;
+#define ORDER_MD 0
+#define ORDER_AMD 1
 static pattern_t g_pat[MAXN + 1];
 
 static int *dupi(const int *a, int n) {
@@ -362,9 +370,292 @@ static void min_degree(int n, const int *Kp, const int *Ki, int *perm) {
   free(done);
 }
 
-static int build_kkt_symbolic(int N) {
+/* Approximate minimum degree ordering of a symmetric pattern (the ordering CasADi's ldl(A, amd=True)
+ * applies before its LDL^T). Restated from the published algorithm -- Amestoy, Davis & Duff, "An
+ * approximate minimum degree ordering algorithm", SIAM J. Matrix Anal. Appl. 17(4), 1996 -- in the form
+ * T. A. Davis gives it as cs_amd (Direct Methods for Sparse Linear Systems, SIAM 2006, section 7.1) with
+ * order 1 (the pattern of A + A^T without its diagonal): a quotient graph of variables and elements,
+ * approximate external degrees |Le \ Lk| from one scan of the element lists, mass elimination,
+ * aggressive element absorption, indistinguishable-variable (supervariable) detection by hashing,
+ * dense rows (degree > max(16, 10 sqrt n)) ordered last, and the assembly tree postordered. Tie-breaks
+ * follow that form: degree lists are LIFO, the pivot is the head of the lowest non-empty list. The
+ * quotient graph gets enough elbow room that it is never compacted (compaction moves lists, not their
+ * order, so the ordering is the same). Kp / Ki: CSC of a symmetric pattern (diagonal allowed, ignored);
+ * perm[k] = the k-th variable eliminated. Returns 0, or -1 on allocation failure. */
+#define AMD_FLIP(i) (-(i) - 2)
+static int amd_clear(int mark, int lemax, int *w, int n) {
+  if (mark < 2 || mark + lemax < 0) {
+    for (int k = 0; k < n; ++k)
+      if (w[k] != 0) w[k] = 1;
+    mark = 2;
+  }
+  return mark;
+}
+static int amd_postorder_dfs(int j, int k, int *head, const int *next, int *post, int *stack) {
+  int top = 0;
+  stack[0] = j;
+  while (top >= 0) {
+    const int p = stack[top];
+    const int i = head[p];
+    if (i == -1) {
+      top--;
+      post[k++] = p;
+    } else {
+      head[p] = next[i];
+      stack[++top] = i;
+    }
+  }
+  return k;
+}
+static int amd_order(int n, const int *Kp, const int *Ki, int *perm) {
+  /* quotient graph storage: the off-diagonal pattern, then room for every element list */
+  int cnz = 0;
+  for (int c = 0; c < n; ++c)
+    for (int q = Kp[c]; q < Kp[c + 1]; ++q) cnz += Ki[q] != c;
+  const long cap = (long)cnz + (long)n * (n + 1) + 16;
+  int *Cp = (int *)malloc(sizeof(int) * (n + 1)), *Ci = (int *)malloc(sizeof(int) * cap);
+  int *W = (int *)malloc(sizeof(int) * 8 * (n + 1)), *P = (int *)malloc(sizeof(int) * (n + 1));
+  if (!Cp || !Ci || !W || !P) { free(Cp); free(Ci); free(W); free(P); return -1; }
+  for (int c = 0, t = 0; c < n; ++c) {
+    Cp[c] = t;
+    for (int q = Kp[c]; q < Kp[c + 1]; ++q)
+      if (Ki[q] != c) Ci[t++] = Ki[q];
+  }
+  Cp[n] = cnz;
+  int *len = W, *nv = W + (n + 1), *next = W + 2 * (n + 1), *head = W + 3 * (n + 1);
+  int *elen = W + 4 * (n + 1), *degree = W + 5 * (n + 1), *w = W + 6 * (n + 1), *hhead = W + 7 * (n + 1);
+  int *last = P; /* last[] shares the output array, as the postorder overwrites it at the end */
+  int dense = (int)fmax(16.0, 10.0 * sqrt((double)n));
+  if (dense > n - 2) dense = n - 2;
+  for (int k = 0; k < n; ++k) len[k] = Cp[k + 1] - Cp[k];
+  len[n] = 0;
+  for (int i = 0; i <= n; ++i) {
+    head[i] = last[i] = next[i] = hhead[i] = -1;
+    nv[i] = 1;
+    w[i] = 1;
+    elen[i] = 0;
+    degree[i] = len[i];
+  }
+  int mark = amd_clear(0, 0, w, n), nel = 0, mindeg = 0, lemax = 0;
+  elen[n] = -2;
+  Cp[n] = -1;
+  w[n] = 0;
+  for (int i = 0; i < n; ++i) { /* degree lists; empty and dense variables leave at once */
+    const int d = degree[i];
+    if (d == 0) {
+      elen[i] = -2;
+      nel++;
+      Cp[i] = -1;
+      w[i] = 0;
+    } else if (d > dense) {
+      nv[i] = 0;
+      elen[i] = -1;
+      nel++;
+      Cp[i] = AMD_FLIP(n);
+      nv[n]++;
+    } else {
+      if (head[d] != -1) last[head[d]] = i;
+      next[i] = head[d];
+      head[d] = i;
+    }
+  }
+  while (nel < n) {
+    int k = -1;
+    for (; mindeg < n && (k = head[mindeg]) == -1; mindeg++) {
+    }
+    if (next[k] != -1) last[next[k]] = -1;
+    head[mindeg] = next[k];
+    const int elenk = elen[k];
+    int nvk = nv[k];
+    nel += nvk;
+    /* the new element Lk: the variables of k's elements and of k's own list */
+    int dk = 0;
+    nv[k] = -nvk;
+    int p = Cp[k];
+    const int pk1 = (elenk == 0) ? p : cnz;
+    int pk2 = pk1;
+    for (int k1 = 1; k1 <= elenk + 1; k1++) {
+      int e, pj, ln;
+      if (k1 > elenk) {
+        e = k;
+        pj = p;
+        ln = len[k] - elenk;
+      } else {
+        e = Ci[p++];
+        pj = Cp[e];
+        ln = len[e];
+      }
+      for (int k2 = 1; k2 <= ln; k2++) {
+        const int i = Ci[pj++];
+        const int nvi = nv[i];
+        if (nvi <= 0) continue;
+        dk += nvi;
+        nv[i] = -nvi;
+        Ci[pk2++] = i;
+        if (next[i] != -1) last[next[i]] = last[i];
+        if (last[i] != -1) next[last[i]] = next[i];
+        else head[degree[i]] = next[i];
+      }
+      if (e != k) {
+        Cp[e] = AMD_FLIP(k);
+        w[e] = 0;
+      }
+    }
+    if (elenk != 0) cnz = pk2;
+    degree[k] = dk;
+    Cp[k] = pk1;
+    len[k] = pk2 - pk1;
+    elen[k] = -2;
+    /* |Le \ Lk| for every element e adjacent to Lk */
+    mark = amd_clear(mark, lemax, w, n);
+    for (int pk = pk1; pk < pk2; pk++) {
+      const int i = Ci[pk];
+      const int eln = elen[i];
+      if (eln <= 0) continue;
+      const int nvi = -nv[i];
+      const int wnvi = mark - nvi;
+      for (int q = Cp[i]; q <= Cp[i] + eln - 1; q++) {
+        const int e = Ci[q];
+        if (w[e] >= mark) w[e] -= nvi;
+        else if (w[e] != 0) w[e] = degree[e] + wnvi;
+      }
+    }
+    /* approximate degrees of the variables of Lk; prune their lists; hash them */
+    for (int pk = pk1; pk < pk2; pk++) {
+      const int i = Ci[pk];
+      const int p1 = Cp[i], p2 = p1 + elen[i] - 1;
+      int pn = p1, d = 0;
+      long h = 0;
+      for (int q = p1; q <= p2; q++) {
+        const int e = Ci[q];
+        if (w[e] != 0) {
+          const int dext = w[e] - mark;
+          if (dext > 0) {
+            d += dext;
+            Ci[pn++] = e;
+            h += e;
+          } else {
+            Cp[e] = AMD_FLIP(k); /* aggressive absorption */
+            w[e] = 0;
+          }
+        }
+      }
+      elen[i] = pn - p1 + 1;
+      const int p3 = pn, p4 = p1 + len[i];
+      for (int q = p2 + 1; q < p4; q++) {
+        const int j = Ci[q];
+        const int nvj = nv[j];
+        if (nvj <= 0) continue;
+        d += nvj;
+        Ci[pn++] = j;
+        h += j;
+      }
+      if (d == 0) { /* mass elimination */
+        Cp[i] = AMD_FLIP(k);
+        const int nvi = -nv[i];
+        dk -= nvi;
+        nvk += nvi;
+        nel += nvi;
+        nv[i] = 0;
+        elen[i] = -1;
+      } else {
+        if (d < degree[i]) degree[i] = d;
+        Ci[pn] = Ci[p3];
+        Ci[p3] = Ci[p1];
+        Ci[p1] = k;
+        len[i] = pn - p1 + 1;
+        const int hb = (int)((h < 0 ? -h : h) % n);
+        next[i] = hhead[hb];
+        hhead[hb] = i;
+        last[i] = hb;
+      }
+    }
+    degree[k] = dk;
+    if (dk > lemax) lemax = dk;
+    mark = amd_clear(mark + lemax, lemax, w, n);
+    /* supervariables: variables of Lk with identical lists (one hash bucket at a time) */
+    for (int pk = pk1; pk < pk2; pk++) {
+      int i = Ci[pk];
+      if (nv[i] >= 0) continue;
+      const int hb = last[i];
+      i = hhead[hb];
+      hhead[hb] = -1;
+      for (; i != -1 && next[i] != -1; i = next[i], mark++) {
+        const int ln = len[i], eln = elen[i];
+        for (int q = Cp[i] + 1; q <= Cp[i] + ln - 1; q++) w[Ci[q]] = mark;
+        int jlast = i;
+        for (int j = next[i]; j != -1;) {
+          int ok = (len[j] == ln) && (elen[j] == eln);
+          for (int q = Cp[j] + 1; ok && q <= Cp[j] + ln - 1; q++)
+            if (w[Ci[q]] != mark) ok = 0;
+          if (ok) {
+            Cp[j] = AMD_FLIP(i);
+            nv[i] += nv[j];
+            nv[j] = 0;
+            elen[j] = -1;
+            j = next[j];
+            next[jlast] = j;
+          } else {
+            jlast = j;
+            j = next[j];
+          }
+        }
+      }
+    }
+    /* back into the degree lists with their external degrees */
+    int pw = pk1;
+    for (int pk = pk1; pk < pk2; pk++) {
+      const int i = Ci[pk];
+      const int nvi = -nv[i];
+      if (nvi <= 0) continue;
+      nv[i] = nvi;
+      int d = degree[i] + dk - nvi;
+      if (d > n - nel - nvi) d = n - nel - nvi;
+      if (head[d] != -1) last[head[d]] = i;
+      next[i] = head[d];
+      last[i] = -1;
+      head[d] = i;
+      if (d < mindeg) mindeg = d;
+      degree[i] = d;
+      Ci[pw++] = i;
+    }
+    nv[k] = nvk;
+    if ((len[k] = pw - pk1) == 0) {
+      Cp[k] = -1;
+      w[k] = 0;
+    }
+    if (elenk != 0) cnz = pw;
+    if ((long)cnz + (long)n >= cap) { free(Cp); free(Ci); free(W); free(P); return -1; }
+  }
+  /* postorder the assembly tree: absorbed variables and elements under their parents */
+  for (int i = 0; i < n; ++i) Cp[i] = AMD_FLIP(Cp[i]);
+  for (int j = 0; j <= n; ++j) head[j] = -1;
+  for (int j = n; j >= 0; j--) {
+    if (nv[j] > 0) continue;
+    next[j] = head[Cp[j]];
+    head[Cp[j]] = j;
+  }
+  for (int e = n; e >= 0; e--) {
+    if (nv[e] <= 0) continue;
+    if (Cp[e] != -1) {
+      next[e] = head[Cp[e]];
+      head[Cp[e]] = e;
+    }
+  }
+  for (int k = 0, i = 0; i <= n; i++)
+    if (Cp[i] == -1) k = amd_postorder_dfs(i, k, head, next, P, w);
+  memcpy(perm, P, sizeof(int) * n); /* P[n] is the dense-row root n */
+  free(Cp); free(Ci); free(W); free(P);
+  return 0;
+}
+
+/* amd_order of an arbitrary symmetric CSC pattern (tests/test_oracle.py pins it on small graphs) */
+int oracle_amd_order(int n, const int *Kp, const int *Ki, int *perm) { return n < 1 ? -1 : amd_order(n, Kp, Ki, perm); }
+
+/* the full KKT pattern of sparse_pdipm_solver.py:412-439 (shared by both orderings) */
+static int build_kkt_pattern(int N) {
   pattern_t *P = &g_pat[N];
-  if (P->ldl_ready) return 0;
+  if (P->kkt_ready) return 0;
   const int nz = 24 * N, m = 16 * N, p = 14 * N, n = nz + 2 * m + p;
   const int cap = 2 * (P->nH + P->nA + P->nG) + 4 * n + 16;
   trip_t *T = (trip_t *)malloc(sizeof(trip_t) * cap);
@@ -411,54 +702,82 @@ static int build_kkt_symbolic(int N) {
   }
   for (int c = 0; c < n; ++c) P->Kp[c + 1] += P->Kp[c];
   free(T);
-  P->Perm = (int *)malloc(sizeof(int) * n);
-  P->Pinv = (int *)malloc(sizeof(int) * n);
-  min_degree(n, P->Kp, P->Ki, P->Perm);
-  for (int k = 0; k < n; ++k) P->Pinv[P->Perm[k]] = k;
-  /* ldl_symbolic (elimination tree + column counts) on the permuted matrix */
-  P->Lp = (int *)malloc(sizeof(int) * (n + 1));
-  P->Parent = (int *)malloc(sizeof(int) * n);
+  P->kkt_ready = 1;
+  return 0;
+}
+
+/* ordering `order` of the KKT and ldl_symbolic (elimination tree + column counts) on the permuted
+ * matrix. Built once per (N, order), before any batch loop (the batched entry points are parallel). */
+static int build_kkt_symbolic_ord(int N, int order) {
+  if (order != ORDER_MD && order != ORDER_AMD) return -1;
+  if (build_kkt_pattern(N)) return -1;
+  pattern_t *P = &g_pat[N];
+  if (P->sym[order].ready) return 0;
+  const int n = P->n;
+  int *Perm = (int *)malloc(sizeof(int) * n), *Pinv = (int *)malloc(sizeof(int) * n);
+  if (order == ORDER_MD) min_degree(n, P->Kp, P->Ki, Perm);
+  else if (amd_order(n, P->Kp, P->Ki, Perm)) { free(Perm); free(Pinv); return -1; }
+  for (int k = 0; k < n; ++k) Pinv[k] = -1;
+  for (int k = 0; k < n; ++k) {
+    if (Perm[k] < 0 || Perm[k] >= n || Pinv[Perm[k]] != -1) { free(Perm); free(Pinv); return -1; }
+    Pinv[Perm[k]] = k;
+  }
+  int *Lp = (int *)malloc(sizeof(int) * (n + 1)), *Parent = (int *)malloc(sizeof(int) * n);
   int *Lnz = (int *)malloc(sizeof(int) * n), *Flag = (int *)malloc(sizeof(int) * n);
   for (int k = 0; k < n; ++k) {
-    P->Parent[k] = -1;
+    Parent[k] = -1;
     Flag[k] = k;
     Lnz[k] = 0;
-    const int kk = P->Perm[k];
+    const int kk = Perm[k];
     for (int q = P->Kp[kk]; q < P->Kp[kk + 1]; ++q) {
-      int i = P->Pinv[P->Ki[q]];
+      int i = Pinv[P->Ki[q]];
       if (i < k)
-        for (; Flag[i] != k; i = P->Parent[i]) {
-          if (P->Parent[i] == -1) P->Parent[i] = k;
+        for (; Flag[i] != k; i = Parent[i]) {
+          if (Parent[i] == -1) Parent[i] = k;
           Lnz[i]++;
           Flag[i] = k;
         }
     }
   }
-  P->Lp[0] = 0;
-  for (int k = 0; k < n; ++k) P->Lp[k + 1] = P->Lp[k] + Lnz[k];
+  Lp[0] = 0;
+  for (int k = 0; k < n; ++k) Lp[k + 1] = Lp[k] + Lnz[k];
   free(Lnz);
   free(Flag);
-  P->ldl_ready = 1;
+  P->sym[order].Perm = Perm;
+  P->sym[order].Pinv = Pinv;
+  P->sym[order].Lp = Lp;
+  P->sym[order].Parent = Parent;
+  P->sym[order].ready = 1;
   return 0;
 }
+static int build_kkt_symbolic(int N) { return build_kkt_symbolic_ord(N, ORDER_MD); }
 
 int oracle_prepare_solver(int N) {
   if (N < 1 || N > MAXN || !g_pat[N].set) return -1;
   return build_kkt_symbolic(N);
 }
 
-int oracle_kkt_stats(int N, int *n, int *nnzK, int *nnzL) {
-  if (oracle_prepare_solver(N)) return -1;
+/* the KKT size, its nonzeros and those of L under ordering `order` (0 exact minimum degree, 1 AMD) */
+int oracle_kkt_stats_ord(int N, int order, int *n, int *nnzK, int *nnzL) {
+  if (N < 1 || N > MAXN || !g_pat[N].set || build_kkt_symbolic_ord(N, order)) return -1;
   *n = g_pat[N].n;
   *nnzK = g_pat[N].nnzK;
-  *nnzL = g_pat[N].Lp[g_pat[N].n];
+  *nnzL = g_pat[N].sym[order].Lp[g_pat[N].n];
   return 0;
+}
+int oracle_kkt_stats(int N, int *n, int *nnzK, int *nnzL) { return oracle_kkt_stats_ord(N, ORDER_MD, n, nnzK, nnzL); }
+
+/* the elimination order itself (perm[k] = KKT row eliminated k-th); returns n or -1 */
+int oracle_kkt_order(int N, int order, int *perm) {
+  if (N < 1 || N > MAXN || !g_pat[N].set || build_kkt_symbolic_ord(N, order)) return -1;
+  memcpy(perm, g_pat[N].sym[order].Perm, sizeof(int) * g_pat[N].n);
+  return g_pat[N].n;
 }
 
 /* column pointers of L (nnz per column = Lp[j+1] - Lp[j]) for flop accounting */
 int oracle_kkt_lp(int N, int *Lp_out) {
   if (oracle_prepare_solver(N)) return -1;
-  memcpy(Lp_out, g_pat[N].Lp, sizeof(int) * (g_pat[N].n + 1));
+  memcpy(Lp_out, g_pat[N].sym[ORDER_MD].Lp, sizeof(int) * (g_pat[N].n + 1));
   return g_pat[N].n;
 }
 
@@ -468,7 +787,10 @@ typedef struct {
 } ldl_work;
 
 /* ldl_numeric (up-looking LDL^T, no pivoting) */
-static int ldl_numeric(const pattern_t *P, ldl_work *w) {
+typedef struct {
+  const int *Perm, *Pinv, *Lp, *Parent;
+} sym_ref;
+static int ldl_numeric(const pattern_t *P, sym_ref S, ldl_work *w) {
   const int n = P->n;
   int fail = 0;  /* first zero pivot (1-based); the factorisation still runs to the end, so every column
                     of L has its pattern and ldl_solve stays in bounds (the values are then inf / NaN) */
@@ -477,13 +799,13 @@ static int ldl_numeric(const pattern_t *P, ldl_work *w) {
     int top = n;
     w->Flag[k] = k;
     w->Lnz[k] = 0;
-    const int kk = P->Perm[k];
+    const int kk = S.Perm[k];
     for (int q = P->Kp[kk]; q < P->Kp[kk + 1]; ++q) {
-      int i = P->Pinv[P->Ki[q]];
+      int i = S.Pinv[P->Ki[q]];
       if (i <= k) {
         w->Y[i] += w->Kx[q];
         int len;
-        for (len = 0; w->Flag[i] != k; i = P->Parent[i]) {
+        for (len = 0; w->Flag[i] != k; i = S.Parent[i]) {
           w->Pattern[len++] = i;
           w->Flag[i] = k;
         }
@@ -496,9 +818,9 @@ static int ldl_numeric(const pattern_t *P, ldl_work *w) {
       const int i = w->Pattern[top];
       const double yi = w->Y[i];
       w->Y[i] = 0.0;
-      const int p2 = P->Lp[i] + w->Lnz[i];
+      const int p2 = S.Lp[i] + w->Lnz[i];
       int q;
-      for (q = P->Lp[i]; q < p2; q++) w->Y[w->Li[q]] -= w->Lx[q] * yi;
+      for (q = S.Lp[i]; q < p2; q++) w->Y[w->Li[q]] -= w->Lx[q] * yi;
       const double l_ki = yi / w->D[i];
       w->D[k] -= l_ki * yi;
       w->Li[q] = k;
@@ -511,15 +833,15 @@ static int ldl_numeric(const pattern_t *P, ldl_work *w) {
 }
 
 /* ldl_solve: x = P^T L^-T D^-1 L^-1 P b  (b overwritten with the solution) */
-static void ldl_solve(const pattern_t *P, const ldl_work *w, double *b, double *tmp) {
+static void ldl_solve(const pattern_t *P, sym_ref S, const ldl_work *w, double *b, double *tmp) {
   const int n = P->n;
-  for (int k = 0; k < n; ++k) tmp[k] = b[P->Perm[k]];
+  for (int k = 0; k < n; ++k) tmp[k] = b[S.Perm[k]];
   for (int j = 0; j < n; ++j)
-    for (int q = P->Lp[j]; q < P->Lp[j + 1]; ++q) tmp[w->Li[q]] -= w->Lx[q] * tmp[j];
+    for (int q = S.Lp[j]; q < S.Lp[j + 1]; ++q) tmp[w->Li[q]] -= w->Lx[q] * tmp[j];
   for (int j = 0; j < n; ++j) tmp[j] /= w->D[j];
   for (int j = n - 1; j >= 0; --j)
-    for (int q = P->Lp[j]; q < P->Lp[j + 1]; ++q) tmp[j] -= w->Lx[q] * tmp[w->Li[q]];
-  for (int k = 0; k < n; ++k) b[P->Perm[k]] = tmp[k];
+    for (int q = S.Lp[j]; q < S.Lp[j + 1]; ++q) tmp[j] -= w->Lx[q] * tmp[w->Li[q]];
+  for (int k = 0; k < n; ++k) b[S.Perm[k]] = tmp[k];
 }
 
 /* sparse mat-vec helpers with CasADi's column-ordered accumulation */
@@ -564,10 +886,11 @@ static int nonfinite(const double *v, int n) {
 /* sparse_pdipm_multiple_iterations, sparse_pdipm_solver.py:357-534.
  * in : Q_val, G_val, A_val, f, h, b, x, s, z, y        out: x, s, z, y, residuals(4), mu(1)
  * status: NULL, or the status word above. */
-int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const out[6], int *status) {
+static int pdipm_ord(int N, int n_iter, const double *const in[10], double *const out[6], int *status, int order) {
   if (N < 1 || N > MAXN || !g_pat[N].set || n_iter < 1) return -1;
-  if (build_kkt_symbolic(N)) return -1;
+  if (build_kkt_symbolic_ord(N, order)) return -1;
   const pattern_t *P = &g_pat[N];
+  const sym_ref S = {P->sym[order].Perm, P->sym[order].Pinv, P->sym[order].Lp, P->sym[order].Parent};
   const int nz = 24 * N, m = 16 * N, p = 14 * N, n = P->n;
   const double *Hv = in[0], *Gv = in[1], *Av = in[2], *f = in[3], *h = in[4], *b = in[5];
   double *x = (double *)malloc(sizeof(double) * nz), *s = (double *)malloc(sizeof(double) * m);
@@ -577,7 +900,7 @@ int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const
   memcpy(z, in[8], sizeof(double) * m);
   memcpy(y, in[9], sizeof(double) * p);
   ldl_work w;
-  const int nnzL = P->Lp[n];
+  const int nnzL = S.Lp[n];
   w.Kx = (double *)malloc(sizeof(double) * P->nnzK);
   w.Lx = (double *)malloc(sizeof(double) * (nnzL > 0 ? nnzL : 1));
   w.Li = (int *)malloc(sizeof(int) * (nnzL > 0 ? nnzL : 1));
@@ -626,14 +949,14 @@ int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const
     for (int c = 0; c < nz; ++c)
       for (int q = P->Kp[c]; q < P->Kp[c + 1]; ++q)
         if (P->Ki[q] == c && P->Ksrc[q] >= 0) w.Kx[q] += BETA;
-    const int fail = ldl_numeric(P, &w);
+    const int fail = ldl_numeric(P, S, &w);
     if (fail) rc = 2;
     /* affine rhs = [-rx; -(S^-1 (s o z)); -rs; -re] */
     for (int k = 0; k < nz; ++k) sa[k] = -rx[k];
     for (int k = 0; k < m; ++k) sa[nz + k] = -(sinv[k] * (s[k] * z[k]));
     for (int k = 0; k < m; ++k) sa[nz + m + k] = -rs[k];
     for (int k = 0; k < p; ++k) sa[nz + 2 * m + k] = -re[k];
-    ldl_solve(P, &w, sa, tmp);
+    ldl_solve(P, S, &w, sa, tmp);
     const double *dxa = sa, *dsa = sa + nz, *dza = sa + nz + m;
     const double ap = step_length(m, s, dsa), ad = step_length(m, z, dza);
     double sza = 0.0;
@@ -646,7 +969,7 @@ int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const
       const double rcc = s[k] * z[k] + dsa[k] * dza[k] - sigma * mu * 1.0;
       sc[nz + k] = -(sinv[k] * rcc);
     }
-    ldl_solve(P, &w, sc, tmp);
+    ldl_solve(P, S, &w, sc, tmp);
     (void)dxa;
     for (int k = 0; k < n; ++k) sc[k] = sa[k] + sc[k]; /* combined direction */
     const double *dx = sc, *ds = sc + nz, *dz = sc + nz + m, *dy = sc + nz + 2 * m;
@@ -684,6 +1007,10 @@ int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const
   return rc;
 }
 
+int oracle_pdipm_st(int N, int n_iter, const double *const in[10], double *const out[6], int *status) {
+  return pdipm_ord(N, n_iter, in, out, status, ORDER_MD);
+}
+
 int oracle_pdipm(int N, int n_iter, const double *const in[10], double *const out[6]) {
   return oracle_pdipm_st(N, n_iter, in, out, NULL);
 }
@@ -714,10 +1041,12 @@ int oracle_qp_former_batch(int N, int B, const double *const in[17], double *con
   return bad;
 }
 
-int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], double *const out[6], int nthreads,
-                       int *status) {
+/* oracle_pdipm_batch under elimination order `order` (0: the checker's exact minimum degree, 1: AMD,
+ * the ordering of CasADi's ldl) */
+int oracle_pdipm_batch_ord(int N, int n_iter, int B, const double *const in[10], double *const out[6],
+                           int nthreads, int *status, int order) {
   if (N < 1 || N > MAXN || !g_pat[N].set) return -1;
-  if (build_kkt_symbolic(N)) return -1;
+  if (build_kkt_symbolic_ord(N, order)) return -1;
   const pattern_t *P = &g_pat[N];
   const int innz[10] = {P->nH, P->nG, P->nA, 24 * N, 16 * N, 14 * N, 24 * N, 16 * N, 16 * N, 14 * N};
   const int onnz[6] = {24 * N, 16 * N, 16 * N, 14 * N, 4, 1};
@@ -731,9 +1060,14 @@ int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], dou
     double *po[6];
     for (int i = 0; i < 10; ++i) pi[i] = in[i] + (size_t)e * innz[i];
     for (int i = 0; i < 6; ++i) po[i] = out[i] + (size_t)e * onnz[i];
-    bad |= oracle_pdipm_st(N, n_iter, pi, po, status ? status + e : NULL) != 0;
+    bad |= pdipm_ord(N, n_iter, pi, po, status ? status + e : NULL, order) != 0;
   }
   return status ? 0 : bad;
+}
+
+int oracle_pdipm_batch(int N, int n_iter, int B, const double *const in[10], double *const out[6], int nthreads,
+                       int *status) {
+  return oracle_pdipm_batch_ord(N, n_iter, B, in, out, nthreads, status, ORDER_MD);
 }
 
 /* The GPU caller's full MPC step per env (mpc_controller_cusadi.py:99-169): qp_former, then

@@ -1,26 +1,31 @@
 """Randomised parity campaign on the GPU box: HIP path vs the oracle over random configurations.
 
-    python scripts/parity_fuzz.py [SECONDS] [OUT_JSON]     (default 150 s, gpurun_out/parity_fuzz.json)
+    python scripts/parity_fuzz.py [SECONDS] [OUT_JSON_GZ]     (default 150 s, gpurun_out/parity_fuzz.json.gz)
     FUZZ_CASES=n: exactly the first n cases of the fixed random sequence instead of a time budget
     SRBD_LIB=path: another build of libsrbd_mpc.so (A/B of two libraries on the same cases)
-    FUZZ_REFINE=every_iteration: the register kernels' strict refinement mode (srbd_set_refinement(1))
+    FUZZ_POLICIES=name,...: the refinement policies to run every case under (POLICIES below; default
+      "adaptive,strict", the two srbd_set_refinement modes); FUZZ_REFINE=mode: that mode alone (round 5)
+    FUZZ_CCS=1: adds the reference's _ccs entry to the draw (a different random sequence)
 
 Each case draws a horizon N in 1..32, an iteration count K in 1..25, a batch B in 1..300, an entry
 (fused step with y0 in {0, 1}; the solver from the GPU caller's cold init; the solver warm-started
 from the oracle's iterate after K0 iterations -- the reference caller's chained calls; with FUZZ_CCS=1
-also the reference's _ccs entry from a random x_init), a solver path
-(auto / lds / general) and a workload (SURVEY 8d distributions with random tilt, residual scale,
-randomized gait or a random flight / single-support override), runs it through the C-ABI and the
-oracle on the same inputs, and checks every env:
-  * u0 (the controller's output) within 1e-4 relative (north_star);
-  * x, s, z, y within the parity tests' tolerance for K (SOLVER_CASES: 1e-10 / 1e-9 / 1e-7 / 1e-5 at
-    K <= 1 / 5 / 10 / more);
-  an env outside either bound passes only within 4x its own FP64 floor -- the distance between the two
-  CPU restatements (sparse LDL^T oracle, dense LU) on that env, per output and for u0 -- counted as
-  "floor"; otherwise it is a failure.
-One JSON line per case on stdout (progress), the summary in OUT_JSON. Test infrastructure: the oracle is
-the checker only.
+also the reference's _ccs entry from a random x_init), a solver path (auto / lds / general) and a
+workload (SURVEY 8d distributions with random tilt, residual scale, randomized gait or a random flight /
+single-support override), computes the oracle once, runs the HIP call under every policy through the
+C-ABI (the policies act on the register kernels only: a case on the lds or general path, or at N = 1,
+runs once and its result stands for every policy), and records, per policy, EVERY env outside
+  * u0 (the controller's output) within 1e-4 relative (north_star), or
+  * x, s, z, y within the parity tests' tolerance for K (1e-10 / 1e-9 / 1e-7 / 1e-5 at K <= 1 / 5 / 10 /
+    more)
+with its five errors. Such an env passes only within 4x its own FP64 floor -- the spread of the CPU
+restatements on that env -- which is computed offline on the CPU host, for every recorded env, by
+scripts/parity_floor.py (a case is "ok" only when every recorded env of it has been floor-checked and
+passed). Policies outside FUZZ_FULL (default: the two modes) record at most FUZZ_CAP_OTHER = 32 envs per
+case (their worst), enough to reject a variant; the modes record all.
+Test infrastructure: the oracle is the checker only.
 """
+import gzip
 import json
 import os
 import sys
@@ -36,25 +41,54 @@ from biped_pympc_amd.utils.synthetic import make_workload, solver_init  # noqa: 
 from oracle import oracle  # noqa: E402
 from tests._util import rel_err_rows  # noqa: E402
 
-
-MAX_FLOOR = 6
-REFINE = os.environ.get("FUZZ_REFINE", "adaptive")  # _native.refinement mode of the HIP calls
 # FUZZ_CCS=1 adds the reference's _ccs entry (x from x_init, s = max(h - G x, 1), z = 1, y = 0;
 # srbd_pdipm_ccs) to the draw -- a different random sequence from the default one, which
 # tests/golden/make_fuzz_regressions.py replays
 ENTRIES = ["fused", "cold", "warm"] + (["ccs"] if os.environ.get("FUZZ_CCS") == "1" else [])
 
+_C = _native.refine_combined
+_F = _native.refine_affine_first
+_L = _native.refine_affine_last
+# name -> ("mode", srbd_set_refinement mode) or (srbd_set_refinement_policy flags, W threshold)
+POLICIES = {
+    "adaptive": ("mode", 0),                  # the default: affine refined on W >= 1e3 / clamp, combined always
+    "strict": ("mode", 1),                    # affine refined in every iteration
+    "nocomb": (_C(1), 1e3),                   # (a) no combined-direction refinement
+    "nocomb_strict": (_C(1) | 1, 1e3),        # (a) with the affine direction refined in every iteration
+    "lasthalf": (_C(2), 1e3),                 # (b) combined refinement in the last ceil(K/2) iterations
+    "lasthalf_first1": (_C(2) | _F(1), 1e3),
+    "dualrows": (_C(3), 1e3),                 # (c) combined refinement of the dual rows (KKT row 4) only
+    "first1": (_F(1), 1e3),                   # + the affine direction of the first iteration
+    "w1e2": (0, 1e2),                         # the W vote at 1e2
+    "first1_w1e2": (_F(1), 1e2),
+    "first1_last1": (_F(1) | _L(1), 1e3),
+    "first2_w3e2": (_F(2), 3e2),
+}
+FULL = set(os.environ.get("FUZZ_FULL", "adaptive,strict").split(","))
+CAP_OTHER = int(os.environ.get("FUZZ_CAP_OTHER", "32"))
 
-def floor_env(N, K, ins, e):
-    """tests/_util.py dense_floor_env plus the u0 slice: the relative distance between the two CPU
-    restatements (sparse LDL^T oracle, dense-LU oracle/pdipm_dense.py) for x, s, z, y and u0 of env e."""
+
+def policy_ctx(name):
+    kind, v = POLICIES[name]
+    return _native.refinement(("adaptive", "every_iteration")[v]) if kind == "mode" else \
+        _native.refinement_policy(kind, v)
+
+
+def floor_env(N, K, ins, e, dense_once=False):
+    """The FP64 floor of env e, per output x, s, z, y and the u0 slice: the larger distance from the checker
+    (the sparse LDL^T under exact minimum degree) of the two other CPU restatements -- the same LDL^T under
+    AMD, the ordering of the reference's ca.ldl (sparse_pdipm_solver.py:451), and dense LU
+    (oracle/pdipm_dense.py) -- relative per env."""
     from oracle.pdipm_dense import pdipm_dense
     one = [np.asarray(a)[e:e + 1] for a in ins]
-    ref = oracle.pdipm(N, K, one)
-    den = pdipm_dense(N, K, *[a[0] for a in one])
-    fl = [float(rel_err_rows(np.asarray(den[k])[None], ref[k]).max()) for k in range(4)]
+    md = oracle.pdipm(N, K, one, nthreads=1)
+    am = oracle.pdipm(N, K, one, nthreads=1, order="amd")
+    dn = pdipm_dense(N, K, *[a[0] for a in one], factor_once=dense_once)
     u = slice(12 * N, 12 * N + 12)
-    fl.append(float(rel_err_rows(np.asarray(den[0])[None, u], ref[0][:, u]).max()))
+    fl = [max(float(rel_err_rows(np.asarray(dn[k])[None], md[k]).max()), float(rel_err_rows(am[k], md[k]).max()))
+          for k in range(4)]
+    fl.append(max(float(rel_err_rows(np.asarray(dn[0])[None, u], md[0][:, u]).max()),
+                  float(rel_err_rows(am[0][:, u], md[0][:, u]).max())))
     return fl
 
 
@@ -103,6 +137,12 @@ def replay(seed_want):
     return case
 
 
+def replay_all(seed_max):
+    """{seed: case} for every seed up to seed_max, in one pass over the generator."""
+    rng = np.random.default_rng(20261018)
+    return {seed: draw_case(rng) for seed in range(50000, seed_max + 1)}
+
+
 def case_inputs(seed, N, K, B, entry, kw, y0, extra):
     """The case's workload and solver inputs [H, G, A, f, d, b, x, s, z, y] (the start of its iterations)."""
     wl = make_workload(B, N, seed=seed, **kw)
@@ -121,9 +161,9 @@ def case_inputs(seed, N, K, B, entry, kw, y0, extra):
     return wl, [H, G, A, f, d, b, *it]
 
 
-def hip_solve(N, K, entry, path, y0, wl, ins):
+def hip_solve(N, K, entry, path, y0, wl, ins, policy):
     """The case's HIP call: fused step, srbd_pdipm_ccs, or srbd_pdipm from the given iterate."""
-    with _native.solver_path(path), _native.refinement(REFINE):
+    with _native.solver_path(path), policy_ctx(policy):
         if entry == "fused":
             return solver.mpc_solve(cuda(wl.inputs), N, K, y0=y0)
         if entry == "ccs":
@@ -131,81 +171,94 @@ def hip_solve(N, K, entry, path, y0, wl, ins):
         return solver.pdipm(cuda(ins[:6]), cuda(ins[6:]), N, K)
 
 
-def run_case(seed, rng):
+def env_errors(got, ref, N):
+    """(B, 5): x, s, z, y relative errors per env and the u0 slice's."""
+    errs = np.stack([rel_err_rows(got[k], ref[k]) for k in range(4)], 1)
+    u = slice(12 * N, 12 * N + 12)
+    return np.concatenate([errs, rel_err_rows(got[0][:, u], ref[0][:, u])[:, None]], 1)
+
+
+def score(errs, tol):
+    """How far past its bound each env is (> 1: outside the tolerance or the u0 bound)."""
+    return np.maximum((errs[:, :4] / tol).max(1), errs[:, 4] / 1e-4)
+
+
+def run_case(seed, rng, policies):
     N, K, B, entry, path, kw, y0, extra = draw_case(rng)
-    K0 = extra.get("K0", 0)
     wl, ins = case_inputs(seed, N, K, B, entry, kw, y0, extra)
     ref = oracle.mpc_solve(N, K, wl.inputs, y0=y0) if entry == "fused" else oracle.pdipm(N, K, ins)
-    got = hip_solve(N, K, entry, path, y0, wl, ins)
-    torch.cuda.synchronize()
-    got = [t.cpu().numpy() for t in got]
-    u_err = rel_err_rows(got[0][:, 12 * N:12 * N + 12], ref[0][:, 12 * N:12 * N + 12]) if N >= 1 else np.zeros(B)
     tol = tol_for(K)
-    errs = np.stack([rel_err_rows(got[k], ref[k]) for k in range(4)], 1)  # (B, 4)
-    # per env: x, s, z, y within tol (else within 4x the env's FP64 floor), u0 within 1e-4 (else
-    # within 4x its u0 floor: an ill-posed env where the two CPU restatements themselves disagree)
-    floor_envs, fails = 0, []
-    bad = (errs > tol).any(1) | (u_err > 1e-4)
-    above = np.flatnonzero(bad)
-    # the FP64 floor is a dense-LU solve per env (seconds at N = 32): the worst MAX_FLOOR envs are
-    # checked against it, the rest only counted
-    score = np.maximum((errs[above] / tol).max(1), u_err[above] / 1e-4)
-    above = above[np.argsort(-score)]
-    unchecked = int(max(0, len(above) - MAX_FLOOR))
-    u0_fails = 0
-    for e in above[:MAX_FLOOR]:
-        fl = floor_env(N, K, ins, int(e))
-        ok_x = all(errs[e, k] <= max(tol, 4.0 * fl[k]) for k in range(4))
-        ok_u = u_err[e] <= max(1e-4, 4.0 * fl[4])
-        if ok_x and ok_u:
-            floor_envs += 1
-        else:
-            u0_fails += not ok_u
-            fails.append({"env": int(e), "err": errs[e].tolist(), "u0_err": float(u_err[e]), "floor": fl})
-    finite = all(np.all(np.isfinite(g)) for g in got)
-    case = {"seed": seed, "N": N, "K": K, "B": B, "entry": entry, "K0": K0, "path": path, "y0": y0,
-            "tilt": round(kw["tilt"], 3), "residuals": kw["residuals"], "random_gait": kw["random_gait"],
-            "override": "contact_override" in kw, "max_err": float(errs.max()), "tol": tol,
-            "max_u0_rel": float(u_err.max()), "floor_envs": floor_envs, "above_tol_unchecked": unchecked,
-            "fails": fails[:3],
-            "u0_fails": u0_fails, "finite": bool(finite)}
-    case["ok"] = not fails and finite
-    return case
+    cols, first = {}, None
+    sensitive = path == "auto" and N >= 2  # the register kernels: the policies act there only
+    for pol in policies:
+        if first is not None and not sensitive:
+            cols[pol] = {"same_as": first}
+            continue
+        got = hip_solve(N, K, entry, path, y0, wl, ins, pol)
+        torch.cuda.synchronize()
+        got = [t.cpu().numpy() for t in got]
+        errs = env_errors(got, ref, N)
+        sc = score(errs, tol)
+        above = np.flatnonzero(sc > 1.0)
+        above = above[np.argsort(-sc[above])]
+        cap = len(above) if pol in FULL else CAP_OTHER
+        cols[pol] = {"max_err": float(errs[:, :4].max()), "max_u0_rel": float(errs[:, 4].max()),
+                     "n_above": int(len(above)),
+                     "above": [[int(e)] + [float(f"{v:.4g}") for v in errs[e]] for e in above[:cap]],
+                     "finite": bool(all(np.all(np.isfinite(g)) for g in got))}
+        first = first or pol
+    return {"seed": seed, "N": N, "K": K, "B": B, "entry": entry, "K0": extra.get("K0", 0), "path": path,
+            "y0": y0, "tilt": round(kw["tilt"], 3), "residuals": kw["residuals"],
+            "random_gait": kw["random_gait"], "override": "contact_override" in kw, "tol": tol, "cols": cols}
 
 
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 150.0
-    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "parity_fuzz.json")
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "parity_fuzz.json.gz")
+    if os.environ.get("FUZZ_REFINE"):
+        policies = [{"every_iteration": "strict"}.get(os.environ["FUZZ_REFINE"], "adaptive")]
+    else:
+        policies = os.environ.get("FUZZ_POLICIES", "adaptive,strict").split(",")
+    for p in policies:
+        assert p in POLICIES, p
     rng = np.random.default_rng(20261018)
     t0, cases = time.time(), []
     seed = 50000
     max_cases = int(os.environ.get("FUZZ_CASES", "0"))  # a fixed case list (A/B of two libraries)
+    # FUZZ_SEEDS=s1,s2,...: exactly those cases of the sequence (replayed; regression fixtures)
+    only = sorted(int(v) for v in os.environ.get("FUZZ_SEEDS", "").split(",") if v)
+    if only:
+        max_cases = only[-1] - 50000 + 1
     while (len(cases) < max_cases) if max_cases else (time.time() - t0 < budget):
+        if only and seed not in only:
+            draw_case(rng)
+            seed += 1
+            continue
         try:
-            c = run_case(seed, rng)
+            c = run_case(seed, rng, policies)
         except FloatingPointError as ex:  # the checker's own LDL failed (oracle status): no verdict
-            c = {"seed": seed, "oracle_failed": str(ex), "ok": True, "B": 0, "N": 0, "K": 0, "entry": "-",
-                 "path": "-", "max_u0_rel": 0.0, "floor_envs": 0}
+            c = {"seed": seed, "oracle_failed": str(ex), "B": 0, "N": 0, "K": 0, "entry": "-", "path": "-",
+                 "cols": {}}
         cases.append(c)
-        print(json.dumps(c), flush=True)
+        if only and seed == only[-1]:
+            max_cases = len(cases)
+        brief = {p: (v.get("n_above"), f"{v['max_u0_rel']:.1e}") for p, v in c["cols"].items() if "n_above" in v}
+        print(json.dumps({k: c[k] for k in ("seed", "N", "K", "B", "entry", "path")} | {"above": brief}), flush=True)
         seed += 1
     summary = {
-        "cases": len(cases), "envs": int(sum(c["B"] for c in cases)),
-        "failed_cases": [c for c in cases if not c["ok"]],
-        "floor_explained_envs": int(sum(c["floor_envs"] for c in cases)),
-        "above_tol_unchecked_envs": int(sum(c.get("above_tol_unchecked", 0) for c in cases)),
+        "cases": len(cases), "envs": int(sum(c["B"] for c in cases)), "policies": policies,
+        "policy_words": {p: POLICIES[p] for p in policies}, "full_record": sorted(FULL & set(policies)),
         "oracle_failed_cases": int(sum("oracle_failed" in c for c in cases)),
-        "max_u0_rel": max(c["max_u0_rel"] for c in cases),
         "horizons": sorted({c["N"] for c in cases if c["N"]}), "iterations": sorted({c["K"] for c in cases if c["K"]}),
         "by_entry": {e: sum(c["entry"] == e for c in cases) for e in ENTRIES},
         "by_path": {p: sum(c["path"] == p for c in cases) for p in ("auto", "lds", "general")},
-        "seconds": round(time.time() - t0, 1), "build_id": _native.build_id(), "refinement": REFINE,
+        "seconds": round(time.time() - t0, 1), "build_id": _native.build_id(), "ccs": "ccs" in ENTRIES,
     }
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    with open(out, "w") as fh:
-        json.dump({"summary": summary, "cases": cases}, fh, indent=1)
-    print(json.dumps({k: v for k, v in summary.items() if k != "failed_cases"} | {"n_failed": len(summary["failed_cases"])}))
-    return 1 if summary["failed_cases"] else 0
+    with gzip.open(out, "wt") as fh:
+        json.dump({"summary": summary, "cases": cases}, fh)
+    print(json.dumps(summary))
+    return 0
 
 
 if __name__ == "__main__":

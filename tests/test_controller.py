@@ -403,6 +403,11 @@ def test_graphed_step_refuses_stale_or_converted_tensors():
     with pytest.raises(RuntimeError, match="mass"):
         g()
     c.mass = c.mass / 1.1
+    from biped_pympc_amd import _native
+    g = GraphedMPCStep(c)
+    with _native.refinement("every_iteration"):  # the refinement mode is baked into the kernel's arguments
+        with pytest.raises(RuntimeError, match="refinement"):
+            g()
     g = GraphedMPCStep(c)
     c.state_estimate_data.root_position.add_(0.01)  # in-place updates stay fine
     g()

@@ -309,6 +309,56 @@ def test_capped_pool_shared_by_two_streams():
     assert _native.scratch_pool()["slots"] >= 256
 
 
+def test_pool_resized_and_released_while_another_thread_solves():
+    """One host thread solves mixed batches (fallback QPs use the scratch pool) while another resizes
+    and releases the pool: a launch holds the pool from attach to enqueue (srbd_mpc.hip g_pool_rw), so
+    no kernel runs on a freed pool and every solve matches the oracle."""
+    import threading
+    from biped_pympc_amd import _native
+    ins, _ = _mixed_inputs(10, 600, 93)
+    ref = oracle.pdipm(10, 5, ins)
+    dev_in = (_cuda(ins[:6]), _cuda(ins[6:]))
+    outs, errors = [], []
+    torch.cuda.synchronize()
+
+    def solve():
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                for _ in range(24):
+                    outs.append([t.clone() for t in solver.pdipm(*dev_in, 10, 5)[:4]])
+            st.synchronize()
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errors.append(ex)
+
+    def churn():
+        try:
+            for k in range(24):
+                _native.set_scratch_slots(3 if k % 2 == 0 else 0)
+                if k % 3 == 2:
+                    _native.release_device()
+        except Exception as ex:  # noqa: BLE001
+            errors.append(ex)
+
+    try:
+        th = [threading.Thread(target=solve), threading.Thread(target=churn)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=90)
+        assert not any(t.is_alive() for t in th) and not errors, errors
+        torch.cuda.synchronize()
+        assert len(outs) == 24
+        for out in outs:
+            for k in range(4):
+                e = rel_err_rows(out[k].cpu().numpy(), ref[k])
+                assert e.max() <= 1e-7, (k, e.max())
+    finally:
+        _native.set_scratch_slots(0)
+    _native.prepare_device()
+    assert _native.scratch_pool()["slots"] >= 256
+
+
 def _mixed_inputs(N, B, seed=77):
     wl = make_workload(B, N, seed=seed)
     H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)

@@ -181,24 +181,3 @@ def test_sii_entry_order_covers_each_class_once():
     assert all(sparse(e) == 0 for e in order[:21]) and all(sparse(e) > 0 for e in order[21:])
     assert dense_cost(order[:21]) <= 5 and sparse_cost(order[21:]) <= 1
 
-
-def test_pipelined_sii_entry_partition():
-    """The stage-pipelined S_ii build of two-wave QPs (csrc/pdipm_srbd_reg.hpp kPipeEntry /
-    c_pipe_entry, RegCtx::pipe_factor): positions into kSiiOrder, each exactly once; pass A (lanes
-    0..63) takes the 21 dense x dense entries and 43 sparse-index ones, pass B (lanes 0..13) 14 sparse
-    entries whose sparse index sits at foot position 2 (pass B's products use the compile-time slots
-    sym_idx(2, b)); the host copy and the __constant__ copy are the same table."""
-    import re
-    src = open(os.path.join(ROOT, "biped_pympc_amd", "csrc", "srbd_common.hpp")).read()
-    order = [int(v) for v in re.search(r"kSiiOrder\[78\] = \{([^}]*)\}", src).group(1).split(",")]
-    reg = open(os.path.join(ROOT, "biped_pympc_amd", "csrc", "pdipm_srbd_reg.hpp")).read()
-    host = [int(v) for v in re.search(r"kPipeEntry\[78\] = \{([^}]*)\}", reg).group(1).split(",")]
-    dev = [int(v) for v in re.search(r"c_pipe_entry\[78\] = \{([^}]*)\}", reg).group(1).split(",")]
-    assert host == dev and sorted(host) == list(range(78))
-    assert host[:21] == list(range(21))
-
-    def foot_pos(k):  # foot position of the sparse index of entry k (rows {3,4,5,9,10,11} of N)
-        r, c = order[k] & 15, order[k] >> 4
-        return (r if r % 6 >= 3 else c) % 3
-    assert all(k >= 21 for k in host[21:])
-    assert all(foot_pos(k) == 2 for k in host[64:]) and len(host[64:]) == 14

@@ -55,6 +55,57 @@ def test_sparse_ldl_oracle_matches_dense_lu_restatement(K):
             assert rel_err(out[k][e], ref[k]) < 1e-8, (e, k)
 
 
+def _sym_csc(n, edges):
+    cols = [[c] for c in range(n)]
+    for i, j in edges:
+        cols[j].append(i)
+        cols[i].append(j)
+    cols = [sorted(c) for c in cols]
+    return np.cumsum([0] + [len(c) for c in cols]), np.concatenate(cols)
+
+
+def test_amd_ordering_known_answers():
+    """The approximate-minimum-degree restatement (srbd_oracle.c amd_order, the order of CasADi's
+    ldl(A, amd=True)) on graphs traced by hand through the published algorithm (cs_amd form, order 1):
+    a path eliminates from the LIFO head of the degree-1 list (node 5), the last pivot's neighbour is
+    mass-eliminated into it and postordered before it; a dense row (degree > max(16, 10 sqrt n), capped
+    at n - 2) is ordered last, behind the isolated leaves (each its own root)."""
+    assert list(oracle.amd_order(6, *_sym_csc(6, [(i, i + 1) for i in range(5)]))) == [5, 4, 3, 2, 0, 1]
+    assert list(oracle.amd_order(40, *_sym_csc(40, [(0, i) for i in range(1, 40)]))) == list(range(1, 40)) + [0]
+    assert list(oracle.amd_order(5, *_sym_csc(5, [(0, i) for i in range(1, 5)]))) == [1, 2, 3, 4, 0]
+
+
+@pytest.mark.parametrize("N", [1, 2, 10, 20, 32])
+def test_amd_ordering_of_the_kkt(N):
+    """Both KKT orderings are permutations, and AMD's fill stays within 10 % of exact minimum degree's."""
+    md, amd = oracle.kkt_stats(N, "md"), oracle.kkt_stats(N, "amd")
+    perm = oracle.kkt_order(N, "amd")
+    assert sorted(perm.tolist()) == list(range(md["n"]))
+    assert amd["nnz_L"] <= 1.1 * md["nnz_L"]
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_three_restatements_agree_on_the_golden_fixtures(N):
+    """The FP64 floor's three CPU restatements of sparse_pdipm_multiple_iterations -- the checker's
+    sparse LDL^T under exact minimum degree, the same LDL^T under AMD (the ordering of the reference's
+    ca.ldl, sparse_pdipm_solver.py:451, whose rounding path it follows), dense LU with pivoting -- agree
+    pairwise within the parity tests' tolerance for K (1e-10 / 1e-9 / 1e-7 / 1e-5) on every golden env, at
+    both dual inits. Measured: AMD-vs-MD up to 2.8e-11 / 3.9e-10 / 5.9e-9 / 8.9e-9."""
+    z, _ = _golden(N)
+    H, f, A, b, G, d = (z[k] for k in "HfAbGd")
+    for y0 in (1.0, 0.0):
+        it = solver_init(d, N, y0=y0)
+        for K, tol in ((1, 1e-10), (5, 1e-9), (10, 1e-7), (20, 1e-5)):
+            ins = [H, G, A, f, d, b, *it]
+            md = oracle.pdipm(N, K, ins)
+            am = oracle.pdipm(N, K, ins, order="amd")
+            dense = [pdipm_dense(N, K, *[a[e] for a in ins]) for e in range(H.shape[0])]
+            for k in range(4):
+                dn = np.stack([np.asarray(r[k]) for r in dense])
+                for a, b_ in ((am[k], md[k]), (dn, md[k]), (dn, am[k])):
+                    assert rel_err_rows(a, b_).max() <= tol, (y0, K, k)
+
+
 def test_pdipm_converges_to_kkt_point():
     """After many iterations the iterate satisfies the QP's KKT conditions (independent of how the
     Newton systems are factorised): stationarity, primal feasibility, complementarity."""
