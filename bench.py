@@ -689,6 +689,9 @@ def main(argv=None):
                                    + (", randomized gait" if a.random_gait else ", standing gait"),
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
                        "pdipm_iters": K, "qp_dims": [d.nz, d.n_eq, d.n_ineq],
+                       # the register kernels' refinement mode (srbd_set_refinement)
+                       "refinement": {0: "adaptive", 1: "every_iteration"}.get(_native.current_refinement(),
+                                                                               "policy"),
                        "parallelism": f"dp{world}" + (f" (u0 all_gather over {'RCCL' if backend == 'nccl' else backend})"
                                                       if world > 1 else "")},
             # solves/s without the u0 gather (every rank's shard solve alone), N > 1 only

@@ -232,6 +232,7 @@ class refinement:
 
 # srbd_set_refinement_policy's word (include/srbd_mpc.h SRBD_REFINE_*)
 REFINE_AFFINE_ALL = 1
+REFINE_AFFINE_AT_INIT = 2  # at an iterate whose duals are all 1 (a solve's initial iterate)
 
 
 def refine_affine_first(k: int) -> int:
@@ -240,11 +241,6 @@ def refine_affine_first(k: int) -> int:
 
 def refine_affine_last(k: int) -> int:
     return (int(k) & 255) << 16
-
-
-def refine_combined(c: int) -> int:
-    """0 every iteration, 1 never, 2 the last ceil(K / 2) iterations, 3 the dual rows only."""
-    return (int(c) & 3) << 24
 
 
 class refinement_policy:

@@ -54,9 +54,9 @@ struct SolverArgs {
 };
 
 // Refinement policy word of the register kernels (include/srbd_mpc.h SRBD_REFINE_*): bit 0 the affine
-// direction in every iteration, bits 8-15 / 16-23 in the first / last k iterations, bits 24-25 the
-// combined direction's refinement (0 every iteration, 1 never, 2 the last ceil(K / 2), 3 dual rows only)
-constexpr int kRefineAffineAll = 1;
+// direction in every iteration, bit 1 at an iterate whose duals z are all 1 (a solve's initial iterate), bits
+// 8-15 / 16-23 in the first / last k iterations
+constexpr int kRefineAffineAll = 1, kRefineAffineAtInit = 2;
 
 // Per-problem status word (SURVEY.md 5 "failure detection"; the reference has only its clamps,
 // sparse_pdipm_solver.py:466-467,501-515): bit 0 a non-finite value in the returned x, s, z, y or

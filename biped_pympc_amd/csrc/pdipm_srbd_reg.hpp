@@ -26,6 +26,12 @@
 #ifndef SRBD_PHASE_ATTR
 #define SRBD_PHASE_ATTR  // diagnostic builds: __attribute__((noinline)) to read one phase ISA alone
 #endif
+#ifndef SRBD_REFINE_COMBINED
+// the combined direction's refinement: 0 every iteration (product); diagnostic builds only: 1 never, 2 the
+// last ceil(K / 2) iterations, 3 the dual rows (KKT row 4) only -- each measured faster (-16 / -8 / -3 % at
+// N = 10) and each failing several times more parity-campaign cases (round 6)
+#define SRBD_REFINE_COMBINED 0
+#endif
 #ifndef SRBD_SWP_INV
 #define SRBD_SWP_INV 0  // two-wave QPs invert their chain blocks by the software-pipelined sweep: measured slower, off
 #endif
@@ -478,6 +484,11 @@ struct RegCtx {
   __device__ bool block_any(bool p) {
     if constexpr (TPB == 64) return __any(p);
     else return block_reduce<true>(p ? 0.0 : 1.0) < 0.5;
+  }
+  // any(p) || all(q) over the QP's threads in one vote (one reduction for a multi-wave QP)
+  __device__ bool block_any_or_all(bool p, bool q) {
+    if constexpr (TPB == 64) return __any(p) || !__any(!q);
+    else return block_reduce<true>(p ? -1.0 : (q ? 1.0 : 0.0)) != 0.0;
   }
   __device__ double block_min(double v) { return block_reduce<true>(v); }
   // The lane index, re-materialised as an opaque value at the start of every phase: keeps the
@@ -1623,22 +1634,27 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     // W 4.5e3 .. 1.2e8 with s above the clamp drifting to 1e-4 in z, profiles/r05/parity_fuzz.txt).
     // Such iterations also refine the affine direction (the QP is one wave or joined ones: a uniform
     // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations. The refinement policy
-    // (srbd_set_refinement_policy, a kernel argument) adds iterations by position: every one
-    // (srbd_set_refinement(1), as the LDS-resident and general kernels always do), the first k, the last k.
+    // (srbd_set_refinement_policy, a kernel argument) adds iterations by position -- every one
+    // (srbd_set_refinement(1), as the LDS-resident and general kernels always do), the first k, the last k --
+    // and, in mode 0 since round 6, the iterate every solve starts from: all duals z at their initial 1 (the
+    // GPU caller's and the _ccs init), where the cold start's Newton step is largest (round 5's mode 0 left 7 of
+    // its 23 failing _ccs-campaign cases at K = 1 from there). A property of the iterate, not of the
+    // iteration index, so 4 chained 5-iteration calls still equal one 20-iteration call bit for bit.
     bool degen;
     {
       const int l = C.fresh_lane();
-      bool p = false;
+      bool p = false, q = (rpol & kRefineAffineAtInit) != 0;
 #pragma unroll
       for (int t = 0; t < SI; ++t)
-        if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m)
+        if (RegCtx<N>::full_slot(t, m) || l + TPB * t < m) {
           p = p || (C.s[t] <= 1e-8) || (C.z[t] >= rw * C.s[t]);
+          q = q && (C.z[t] == 1.0);
+        }
       degen = (rpol & kRefineAffineAll) || it < ((rpol >> 8) & 255) || it >= n_iter - ((rpol >> 16) & 255) ||
-              C.block_any(p);
+              C.block_any_or_all(p, q);
     }
-    // the combined direction's refinement (policy bits 24-25): every iteration (default), never, the
-    // last ceil(K / 2) iterations, or the dual rows (KKT row 4) only
-    const int cpol = (rpol >> 24) & 3;
+    // the combined direction's refinement (SRBD_REFINE_COMBINED): every iteration in the product
+    constexpr int cpol = SRBD_REFINE_COMBINED;
     const bool refc = cpol == 0 || cpol == 3 || (cpol == 2 && it >= n_iter / 2);
     int ul = C.fresh_lane();
     if (it == n_iter - 1) {  // residual norms of the last iteration (refine_rhs reuses r_x, r_e)

@@ -86,6 +86,9 @@ struct RefinePolicy {
   int flags = 0;
   double w = 0.0;
 };
+// mode 0's policy: the predictor at a solve's initial iterate (all z = 1) and in every iteration with
+// z / s >= 1e3 in some row (round 6)
+constexpr int kDefaultRefineFlags = SRBD_REFINE_AFFINE_AT_INIT;
 constexpr double kDefaultRefineW = 1e3;
 srbd::PerDevice<RefinePolicy> g_refinement;
 int refinement_mode() {
@@ -97,7 +100,7 @@ template <class Args>
 void set_refinement_args(Args& a) {
   const RefinePolicy* p = g_refinement.at(current_device());
   const int mode = p ? p->mode : 0;
-  a.refine_policy = mode == 2 ? p->flags : (mode == 1 ? SRBD_REFINE_AFFINE_ALL : 0);
+  a.refine_policy = mode == 2 ? p->flags : (mode == 1 ? SRBD_REFINE_AFFINE_ALL : kDefaultRefineFlags);
   const double w = mode == 2 ? p->w : kDefaultRefineW;
   a.refine_w = w > 0.0 ? w : INFINITY;
 }
@@ -349,8 +352,8 @@ int srbd_set_refinement(int mode) {
 }
 
 int srbd_set_refinement_policy(int flags, double w) {
-  const int known = SRBD_REFINE_AFFINE_ALL | SRBD_REFINE_AFFINE_FIRST(255) | SRBD_REFINE_AFFINE_LAST(255) |
-                    SRBD_REFINE_COMBINED(3);
+  const int known = SRBD_REFINE_AFFINE_ALL | SRBD_REFINE_AFFINE_AT_INIT | SRBD_REFINE_AFFINE_FIRST(255) |
+                    SRBD_REFINE_AFFINE_LAST(255);
   if ((flags & ~known) != 0 || w != w)
     return set_error(kErrInvalid, "srbd_set_refinement_policy: unknown policy bits or a NaN threshold");
   RefinePolicy* p = g_refinement.at(current_device());

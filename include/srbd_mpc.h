@@ -150,16 +150,18 @@ int srbd_get_refinement(void);
 
 /* Diagnostics (A/B campaigns, scripts/parity_fuzz.py): an explicit refinement policy for the register
  * kernels on the current device, in place of the mode. flags: SRBD_REFINE_AFFINE_ALL (the affine
- * direction in every iteration), SRBD_REFINE_AFFINE_FIRST(k) / SRBD_REFINE_AFFINE_LAST(k) (in the first /
- * last k iterations), and one SRBD_REFINE_COMBINED(c) for the combined direction: 0 every iteration (the
- * modes' choice), 1 never, 2 the last ceil(K / 2) iterations, 3 the dual rows (KKT row 4) only, every
- * iteration. w: the affine vote's W = z / s threshold (mode 0 uses 1e3; w <= 0: no W vote; an s at its
- * clamp always votes). srbd_set_refinement(mode) returns to a mode. Returns 0, or an error for unknown
- * bits or a NaN w. */
+ * direction in every iteration), SRBD_REFINE_AFFINE_AT_INIT (at an iterate whose duals z are all 1: the
+ * initial iterate of the GPU caller's and of the _ccs init), SRBD_REFINE_AFFINE_FIRST(k) /
+ * SRBD_REFINE_AFFINE_LAST(k) (in the first / last k iterations of a call -- position-based: chained calls
+ * then no longer equal one long call); w: the affine vote's W = z / s threshold (w <= 0: no W vote; an s
+ * at its clamp always votes). Mode 0 is SRBD_REFINE_AFFINE_AT_INIT with w = 1e3, mode 1
+ * SRBD_REFINE_AFFINE_ALL. The
+ * combined direction is refined in every iteration whatever the policy. srbd_set_refinement(mode)
+ * returns to a mode. Returns 0, or an error for unknown bits or a NaN threshold. */
 #define SRBD_REFINE_AFFINE_ALL 1
+#define SRBD_REFINE_AFFINE_AT_INIT 2
 #define SRBD_REFINE_AFFINE_FIRST(k) (((k) & 255) << 8)
 #define SRBD_REFINE_AFFINE_LAST(k) (((k) & 255) << 16)
-#define SRBD_REFINE_COMBINED(c) (((c) & 3) << 24)
 int srbd_set_refinement_policy(int flags, double w);
 
 /* Allocates what the solver entry points keep per device -- the general-fallback scratch pool of the

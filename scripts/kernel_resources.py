@@ -22,11 +22,31 @@ def resources(path, want=""):
     return out
 
 
-def body_spills(path, kernel, window=12):
+# instructions of a call's whole-wave register save / restore sequence (the SGPR-spill lanes written or
+# read around it, exec toggles, waits, the other saves), which may sit between a spill and its call
+_CALL_SEQ = ("v_writelane_b32", "v_readlane_b32", "s_nop", "s_or_saveexec_b64", "s_mov_b64 exec",
+             "s_waitcnt", "scratch_store_dword", "scratch_load_dword", "; implicit-def",
+             "v_mov_b32_e32 v0,", "v_mov_b32_e32 v1,", "v_mov_b64_e32 v[0:1],")  # (the call's return value)
+
+
+def _call_adjacent(body, i, step, calls):
+    j = i + step
+    while 0 <= j < len(body):
+        if j in calls:
+            return True
+        t = body[j].strip()
+        if not t or not t.startswith(_CALL_SEQ):
+            return False
+        j += step
+    return False
+
+
+def body_spills(path, kernel):
     """VGPR spill / reload instructions of `kernel` (mangled name) outside the save / restore sequence of
-    a call: a spill followed by an s_swappc_b64 within `window` lines, or a reload preceded by one, is
-    the caller keeping a register across the call (the in-launch fallback's: the whole-wave SGPR-spill
-    register it must save around any call) and runs only on that path. Returns the other lines."""
+    a call: a spill followed by an s_swappc_b64, or a reload preceded by one, with nothing but that
+    sequence's own instructions in between (_CALL_SEQ) is the caller keeping a register across the call
+    (the in-launch fallback's: the whole-wave SGPR-spill registers it must save around any call) and runs
+    only on that path. Returns the other lines."""
     body, on = [], False
     for line in open(path):
         if line.startswith(kernel + ":"):
@@ -35,12 +55,12 @@ def body_spills(path, kernel, window=12):
             break
         if on:
             body.append(line.rstrip("\n"))
-    calls = [i for i, l in enumerate(body) if "s_swappc_b64" in l]
+    calls = {i for i, l in enumerate(body) if "s_swappc_b64" in l}
     out = []
     for i, l in enumerate(body):
-        if "Folded Spill" in l and not any(0 < j - i <= window for j in calls):
+        if "Folded Spill" in l and not _call_adjacent(body, i, 1, calls):
             out.append(l.strip())
-        elif "Folded Reload" in l and not any(0 < i - j <= window for j in calls):
+        elif "Folded Reload" in l and not _call_adjacent(body, i, -1, calls):
             out.append(l.strip())
     return out
 

@@ -46,50 +46,60 @@ from tests._util import rel_err_rows  # noqa: E402
 # tests/golden/make_fuzz_regressions.py replays
 ENTRIES = ["fused", "cold", "warm"] + (["ccs"] if os.environ.get("FUZZ_CCS") == "1" else [])
 
-_C = _native.refine_combined
 _F = _native.refine_affine_first
 _L = _native.refine_affine_last
-# name -> ("mode", srbd_set_refinement mode) or (srbd_set_refinement_policy flags, W threshold)
+# name -> ("mode", srbd_set_refinement mode) or (srbd_set_refinement_policy flags, W threshold[, alpha])
 POLICIES = {
-    "adaptive": ("mode", 0),                  # the default: affine refined on W >= 1e3 / clamp, combined always
-    "strict": ("mode", 1),                    # affine refined in every iteration
-    "nocomb": (_C(1), 1e3),                   # (a) no combined-direction refinement
-    "nocomb_strict": (_C(1) | 1, 1e3),        # (a) with the affine direction refined in every iteration
-    "lasthalf": (_C(2), 1e3),                 # (b) combined refinement in the last ceil(K/2) iterations
-    "lasthalf_first1": (_C(2) | _F(1), 1e3),
-    "dualrows": (_C(3), 1e3),                 # (c) combined refinement of the dual rows (KKT row 4) only
-    "first1": (_F(1), 1e3),                   # + the affine direction of the first iteration
-    "w1e2": (0, 1e2),                         # the W vote at 1e2
-    "first1_w1e2": (_F(1), 1e2),
+    "adaptive": ("mode", 0),            # the default: affine refined at the initial iterate (all z = 1), W >= 1e3, clamp
+    "strict": ("mode", 1),              # the affine direction refined in every iteration
+    "w1e3": (0, 1e3),                   # round 5's mode 0: W >= 1e3 / clamp only
+    "init_w1e3": (2, 1e3),              # = mode 0 since round 6
+    "first1": (_F(1), 1e3),             # the first iteration of every call (position-based)
+    "first2": (_F(2), 1e3),
     "first1_last1": (_F(1) | _L(1), 1e3),
-    "first2_w3e2": (_F(2), 3e2),
+    "w1e2": (0, 1e2),
+    "w1e4": (0, 1e4),
+    "first1_w1e2": (_F(1), 1e2),
+    "first1_w3e2": (_F(1), 3e2),
+    "first1_w3e3": (_F(1), 3e3),
+    "first1_w1e4": (_F(1), 1e4),
 }
+# Measured in round 6 on builds of their own (profiles/r06/), rejected: the combined direction
+# unrefined, refined in the last ceil(K / 2) iterations only, or in its dual rows only (SRBD_REFINE_COMBINED =
+# 1 / 2 / 3), and a trigger on the previous combined step length
 FULL = set(os.environ.get("FUZZ_FULL", "adaptive,strict").split(","))
 CAP_OTHER = int(os.environ.get("FUZZ_CAP_OTHER", "32"))
 
 
 def policy_ctx(name):
-    kind, v = POLICIES[name]
-    return _native.refinement(("adaptive", "every_iteration")[v]) if kind == "mode" else \
-        _native.refinement_policy(kind, v)
+    kind, *v = POLICIES[name]
+    return _native.refinement(("adaptive", "every_iteration")[v[0]]) if kind == "mode" else \
+        _native.refinement_policy(kind, *v)
 
 
-def floor_env(N, K, ins, e, dense_once=False):
-    """The FP64 floor of env e, per output x, s, z, y and the u0 slice: the larger distance from the checker
-    (the sparse LDL^T under exact minimum degree) of the two other CPU restatements -- the same LDL^T under
-    AMD, the ordering of the reference's ca.ldl (sparse_pdipm_solver.py:451), and dense LU
-    (oracle/pdipm_dense.py) -- relative per env."""
+def floor_parts(N, K, ins, e, dense_once=False):
+    """Env e's distances from the checker (the sparse LDL^T under exact minimum degree) of the two other CPU
+    restatements, per output x, s, z, y and the u0 slice, relative per env: {"dense": dense LU
+    (oracle/pdipm_dense.py), "amd": the same LDL^T under AMD, the ordering of the reference's ca.ldl
+    (sparse_pdipm_solver.py:451)}."""
     from oracle.pdipm_dense import pdipm_dense
     one = [np.asarray(a)[e:e + 1] for a in ins]
     md = oracle.pdipm(N, K, one, nthreads=1)
     am = oracle.pdipm(N, K, one, nthreads=1, order="amd")
     dn = pdipm_dense(N, K, *[a[0] for a in one], factor_once=dense_once)
+    dn = [np.asarray(v)[None] for v in dn[:4]]
     u = slice(12 * N, 12 * N + 12)
-    fl = [max(float(rel_err_rows(np.asarray(dn[k])[None], md[k]).max()), float(rel_err_rows(am[k], md[k]).max()))
-          for k in range(4)]
-    fl.append(max(float(rel_err_rows(np.asarray(dn[0])[None, u], md[0][:, u]).max()),
-                  float(rel_err_rows(am[0][:, u], md[0][:, u]).max())))
-    return fl
+
+    def dist(o):
+        return [float(rel_err_rows(o[k], md[k]).max()) for k in range(4)] + \
+               [float(rel_err_rows(o[0][:, u], md[0][:, u]).max())]
+    return {"dense": dist(dn), "amd": dist(am)}
+
+
+def floor_env(N, K, ins, e, dense_once=False):
+    """The FP64 floor of env e: per output, the larger of floor_parts' two distances."""
+    fp = floor_parts(N, K, ins, e, dense_once)
+    return [max(a, b) for a, b in zip(fp["dense"], fp["amd"])]
 
 
 def tol_for(K):

@@ -4,8 +4,9 @@ Envs that scripts/parity_fuzz.py (the randomised parity campaign, round 5) found
 trajectory on the register kernels, replayed from the campaign's fixed random sequence: per env the
 solver inputs (the QP H, G, A, f, d, b and the starting iterate x, s, z, y -- the GPU caller's cold init,
 or the oracle's iterate after K0 iterations for a warm case), the iteration count K, the oracle's
-outputs after K iterations, and the FP64 floor of each output (x, s, z, y, u0): the distance between the
-two CPU restatements, the sparse LDL^T oracle and oracle/pdipm_dense.py (dense LU).
+outputs after K iterations, and the FP64 floor of each output (x, s, z, y, u0): the larger distance from
+the checker (sparse LDL^T, exact minimum degree) of the two other CPU restatements, the same LDL^T under
+AMD (the ordering of the reference's ca.ldl) and oracle/pdipm_dense.py (dense LU).
 
   group "adaptive": iterates at W = z / s of 4.5e3 .. 1.2e8 -- a few of them with every s above the 1e-8
     clamp -- where the unrefined predictor let the trajectory drift 1e2 .. 1e6 x the floor (z up to 2.9e-4
@@ -14,8 +15,11 @@ two CPU restatements, the sparse LDL^T oracle and oracle/pdipm_dense.py (dense L
     explicit-inverse Schur complement's own rounding), at the floor with srbd_set_refinement(1);
   group "stiff": from the campaign with the _ccs entry, envs whose z sat 1e3 .. 4e5 x the floor at clamped
     rows in the strict mode on the register, LDS-resident or general kernels (the path is stored) until the
-    foot blocks were applied through LDL^T solves.
-tests/test_gpu_parity.py::test_fuzz_regressions runs both groups.
+    foot blocks were applied through LDL^T solves (DESIGN.md 3.3);
+  group "unchecked": the round-5 _ccs campaign's cases marked ok with above-tolerance envs it never
+    floor-checked (seeds 52840, 53348, 55400, 56036 -- the last 6.3e-3 off in u0 on the LDS-resident kernel),
+    their two worst envs each, checked since by scripts/parity_floor.py (profiles/r06/); both modes.
+tests/test_gpu_parity.py::test_fuzz_regressions runs the groups.
 """
 import os
 import sys
@@ -37,6 +41,9 @@ STRICT = [(50758, 116), (50870, 51), (51078, 182), (50814, 129), (50944, 98), (5
 # the _ccs campaign's sequence (FUZZ_CCS=1): envs whose z sat 1e3..4e5 x the floor at clamped rows (W = z / s
 # ~ 1e7..1e8) on the path named, in the strict mode, before the LDL^T foot-block solves
 STIFF = [(54319, 67), (53918, 121), (50149, 2), (50902, 51), (51320, 64), (55147, 83)]
+# the _ccs sequence too: the round-5 campaign's ok cases with unchecked envs above the tolerance
+UNCHECKED = [(52840, 110), (52840, 186), (53348, 189), (53348, 142), (55400, 83), (55400, 223), (56036, 17),
+             (56036, 76)]
 
 
 PATHS = {"auto": 0, "general": 1, "lds": 2}
@@ -45,8 +52,8 @@ PATHS = {"auto": 0, "general": 1, "lds": 2}
 def main():
     out = {}
     default_entries = list(pf.ENTRIES)
-    for group, pairs in (("adaptive", ADAPTIVE), ("strict", STRICT), ("stiff", STIFF)):
-        pf.ENTRIES[:] = default_entries + (["ccs"] if group == "stiff" else [])
+    for group, pairs in (("adaptive", ADAPTIVE), ("strict", STRICT), ("stiff", STIFF), ("unchecked", UNCHECKED)):
+        pf.ENTRIES[:] = default_entries + (["ccs"] if group in ("stiff", "unchecked") else [])
         for i, (seed, env) in enumerate(pairs):
             N, K, B, entry, path, kw, y0, extra = pf.replay(seed)
             _, ins = pf.case_inputs(seed, N, K, B, entry, kw, y0, extra)

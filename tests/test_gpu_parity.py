@@ -591,13 +591,16 @@ def test_fuzz_regressions(mode):
     mode must hold them within 4x their floor. Group "strict": envs 5 .. 400 x the floor in the adaptive
     mode, at the floor when every iteration refines its predictor (srbd_set_refinement(1)). Group "stiff"
     (strict mode, on the solver path each env failed on): z 1e3 .. 4e5 x the floor at clamped rows until
-    the foot blocks were applied through LDL^T solves. Per output
+    the foot blocks were applied through LDL^T solves. Group "unchecked" (both modes): the round-5 _ccs
+    campaign's ok cases whose above-tolerance envs it never floor-checked (seed 56036: 6.3e-3 in u0 on the
+    LDS-resident kernel), floor-checked since (scripts/parity_floor.py). The floor: the larger distance of the
+    AMD-ordered LDL^T and dense LU from the checker. Per output
     x, s, z, y: max(the K tolerance, 4 x floor); u0: max(U0_TOL, 4 x its floor)."""
     from biped_pympc_amd import _native
     z = np.load(os.path.join(GOLDEN, "fuzz_regressions.npz"))
-    groups = ("adaptive",) if mode == "adaptive" else ("adaptive", "strict", "stiff")
+    groups = ("adaptive", "unchecked") if mode == "adaptive" else ("adaptive", "strict", "stiff", "unchecked")
     keys = sorted({k.split("_")[0] for k in z.files if k.startswith(groups)})
-    assert len(keys) == (8 if mode == "adaptive" else 21)
+    assert len(keys) == (16 if mode == "adaptive" else 29)
     paths = {v: k for k, v in _native.SOLVER_PATHS.items()}
     for key in keys:
         N, K, seed, env, path = (int(v) for v in z[f"{key}_NK"])
@@ -636,6 +639,51 @@ def test_refinement_mode_is_per_call_and_exact():
         assert rel_err_rows(b[k].cpu().numpy(), ref[k]).max() <= dict(SOLVER_CASES)[K]
     with pytest.raises(RuntimeError):
         _native.check(_native.lib().srbd_set_refinement(2), "srbd_set_refinement")
+
+
+@pytest.mark.parametrize("N", [10, 20, 5])
+def test_refinement_policy_words(N):
+    """srbd_set_refinement_policy: the word of mode 0 (the predictor at the initial iterate, all z = 1, + the
+    W >= 1e3 vote) and of mode 1 (every iteration) reproduce the modes bit for bit on the fused step and the
+    CCS solver; round 5's mode 0 (the W vote alone) differs from today's and stays within the tolerance, and
+    so does a position-based word (the first iteration of every call); unknown bits and a NaN threshold are
+    refused; leaving the context returns to mode 0."""
+    from biped_pympc_amd import _native
+    K, B = 10, 128
+    wl = make_workload(B, N, seed=4343, random_gait=True)
+    ins = _cuda(wl.inputs)
+    H, f, A, b, G, d = oracle.qp_former(N, wl.inputs)
+    qp = _cuda([H, G, A, f, d, b])
+
+    def both():
+        fused = [t.clone() for t in solver.mpc_solve(ins, N, K)[:4]]
+        ccs = [t.clone() for t in solver.pdipm(qp, None, N, K)[:4]]
+        torch.cuda.synchronize()
+        return fused + ccs
+    mode0 = both()
+    with _native.refinement("every_iteration"):
+        mode1 = both()
+    with _native.refinement_policy(_native.REFINE_AFFINE_AT_INIT, 1e3):
+        assert _native.current_refinement() == 2
+        p0 = both()
+    with _native.refinement_policy(_native.refine_affine_first(1), 1e3):
+        f1 = both()
+    with _native.refinement_policy(_native.REFINE_AFFINE_ALL, 1e3):
+        p1 = both()
+    with _native.refinement_policy(0, 1e3):
+        r5 = both()
+    assert _native.current_refinement() == 0
+    assert all(torch.equal(x, y) for x, y in zip(mode0, p0))
+    assert all(torch.equal(x, y) for x, y in zip(mode1, p1))
+    assert not all(torch.equal(x, y) for x, y in zip(mode0, r5))
+    ref = oracle.mpc_solve(N, K, wl.inputs)
+    for k in range(4):
+        assert rel_err_rows(r5[k].cpu().numpy(), ref[k]).max() <= dict(SOLVER_CASES)[K]
+        assert rel_err_rows(f1[k].cpu().numpy(), ref[k]).max() <= dict(SOLVER_CASES)[K]
+    L = _native.lib()
+    assert L.srbd_set_refinement_policy(1 << 24, 1e3) != 0 and "unknown policy bits" in _native.last_error()
+    assert L.srbd_set_refinement_policy(0, float("nan")) != 0
+    assert _native.current_refinement() == 0
 
 
 def test_empty_batch_is_a_no_op():
