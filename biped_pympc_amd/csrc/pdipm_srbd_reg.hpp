@@ -1627,13 +1627,13 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
-    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (1e3 by default), e.g. an s
+    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (5e3 in mode 0), e.g. an s
     // at or near its 1e-8 clamp (sparse_pdipm_solver.py:520) -- is where the reduced solve's affine
     // ds, dz lose digits; their error enters sigma and the corrector, and the trajectory drifts from the
     // reference's (profiles/r02/refinement_4row.txt; round 5: scripts/parity_fuzz.py found iterates at
     // W 4.5e3 .. 1.2e8 with s above the clamp drifting to 1e-4 in z, profiles/r05/parity_fuzz.txt).
     // Such iterations also refine the affine direction (the QP is one wave or joined ones: a uniform
-    // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations. The refinement policy
+    // branch); the bench workload has W >= 1e3 in ~4 % of its QP iterations (round 5's mode 0). The refinement policy
     // (srbd_set_refinement_policy, a kernel argument) adds iterations by position -- every one
     // (srbd_set_refinement(1), as the LDS-resident and general kernels always do), the first k, the last k --
     // and, in mode 0 since round 6, the iterate every solve starts from: all duals z at their initial 1 (the
