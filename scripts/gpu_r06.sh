@@ -8,6 +8,7 @@
 #   ccs      the _ccs-sequence campaign, $CCS_SECONDS (420) s, the same policies
 #   bench    the default bench line and the driver-form run
 #   ab       alternating bench runs against $AB_LIB (default ab/libsrbd_mpc_r05.so), N = 10 and 20
+#   seeds    chosen campaign cases ($SEEDS_DEFAULT, $SEEDS_CCS) under each library of $SEEDS_LIBS
 #   profile  rocprofv3 kernel stats of the bench command, PMC traffic and SQ passes, the configs, smoke,
 #            the two-rank launcher rehearsal on one device over gloo
 # The campaigns' outputs are floor-checked afterwards on the CPU host (scripts/parity_floor.py).
@@ -35,6 +36,21 @@ for step in ${STEPS:-tests}; do
       FUZZ_CCS=1 FUZZ_POLICIES=$POL timeout -k 10 $(( ${CCS_SECONDS:-420} + 300 )) python -u scripts/parity_fuzz.py \
         ${CCS_SECONDS:-420} $O/fuzz_ccs.json.gz > $O/fuzz_ccs.log 2>&1 || { tail -30 $O/fuzz_ccs.log; exit 1; }
       tail -1 $O/fuzz_ccs.log | cut -c1-600 ;;
+    seeds)
+      # chosen cases of both sequences (SEEDS_DEFAULT / SEEDS_CCS) under each library of SEEDS_LIBS ("product"
+      # = the in-tree build), both modes: parity_fuzz.py's FUZZ_SEEDS replay
+      for lib in ${SEEDS_LIBS:-product}; do
+        tag=$(basename ${lib%.so})
+        [ "$lib" = product ] && lib=
+        for seq in default ccs; do
+          seeds=$SEEDS_DEFAULT; cc=0
+          [ $seq = ccs ] && seeds=$SEEDS_CCS && cc=1
+          [ -z "$seeds" ] && continue
+          SRBD_LIB=$lib FUZZ_CCS=$cc FUZZ_SEEDS=$seeds FUZZ_POLICIES=$POL timeout -k 10 300 python -u scripts/parity_fuzz.py 0 \
+            $O/seeds_${seq}_$tag.json.gz > $O/seeds_${seq}_$tag.log 2>&1 || { tail -30 $O/seeds_${seq}_$tag.log; exit 1; }
+        done
+      done
+      ls $O/seeds_* ;;
     bench)
       timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
       timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $O/bench_driver_form.json 2> $O/bench_driver_form.err || exit 1
