@@ -6,6 +6,7 @@
     FUZZ_POLICIES=name,...: the refinement policies to run every case under (POLICIES below; default
       "adaptive,strict", the two srbd_set_refinement modes); FUZZ_REFINE=mode: that mode alone (round 5)
     FUZZ_CCS=1: adds the reference's _ccs entry to the draw (a different random sequence)
+    FUZZ_SEEDS=s1,s2,...: exactly those cases of the sequence (replayed); FUZZ_FULL / FUZZ_CAP_OTHER: below
 
 Each case draws a horizon N in 1..32, an iteration count K in 1..25, a batch B in 1..300, an entry
 (fused step with y0 in {0, 1}; the solver from the GPU caller's cold init; the solver warm-started
