@@ -77,9 +77,9 @@ int solver_path() {
 }
 
 // Refinement policy per device (srbd_set_refinement / srbd_set_refinement_policy). Mode 0 (default):
-// the affine direction on ill-conditioned iterates (z / s >= 1e3 in some row, or an s at its clamp),
-// the combined one in every iteration; mode 1: both in every iteration; mode 2: a policy word set by
-// srbd_set_refinement_policy. Read by the register kernels only (the LDS-resident and general kernels
+// the affine direction at a solve's initial iterate and on ill-conditioned iterates (the policy word
+// below), the combined one in every iteration; mode 1: both in every iteration; mode 2: a policy word set
+// by srbd_set_refinement_policy. Read by the register kernels only (the LDS-resident and general kernels
 // refine both directions in every iteration).
 struct RefinePolicy {
   int mode = 0;
