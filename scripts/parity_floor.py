@@ -173,8 +173,8 @@ def main():
                 continue
             bad = st["fails"] or not st["finite"]
             failed_dense += bool(st.get("fails_dense", 0) or not st["finite"])
-            for f in st["fails"]:
-                big += (f["err"][0] > 1e-4 or f["err"][4] > 1e-4)
+            for f in st["fails"]:  # over 1e-4 in x or u0 AND beyond 4x the floor in that same output
+                big += any(f["err"][k] > max(1e-4, 4.0 * f["floor"][k]) for k in (0, 4))
             if bad:
                 worst = max(worst, max(f["ratio"] for f in st["fails"]) if st["fails"] else float("inf"))
                 failed.append({k: c[k] for k in ("seed", "N", "K", "B", "entry", "K0", "path", "y0")} |
