@@ -7,6 +7,8 @@
       "adaptive,strict", the two srbd_set_refinement modes); FUZZ_REFINE=mode: that mode alone (round 5)
     FUZZ_CCS=1: adds the reference's _ccs entry to the draw (a different random sequence)
     FUZZ_SEEDS=s1,s2,...: exactly those cases of the sequence (replayed); FUZZ_FULL / FUZZ_CAP_OTHER: below
+    FUZZ_ROWS=1: also the HIP x, s, z, y rows of every recorded env of the full-record policies, in
+      OUT_JSON_GZ's name + .rows.npz (keys "<policy>/<seed>/<env>/<x|s|z|y>"; large: for replays of chosen seeds)
 
 Each case draws a horizon N in 1..32, an iteration count K in 1..25, a batch B in 1..300, an entry
 (fused step with y0 in {0, 1}; the solver from the GPU caller's cold init; the solver warm-started
@@ -198,6 +200,9 @@ def score(errs, tol):
     return np.maximum((errs[:, :4] / tol).max(1), errs[:, 4] / 1e-4)
 
 
+ROWS = {}  # FUZZ_ROWS=1: "<policy>/<seed>/<env>/<x|s|z|y>" -> the HIP row
+
+
 def run_case(seed, rng, policies):
     N, K, B, entry, path, kw, y0, extra = draw_case(rng)
     wl, ins = case_inputs(seed, N, K, B, entry, kw, y0, extra)
@@ -217,6 +222,10 @@ def run_case(seed, rng, policies):
         above = np.flatnonzero(sc > 1.0)
         above = above[np.argsort(-sc[above])]
         cap = len(above) if pol in FULL else CAP_OTHER
+        if os.environ.get("FUZZ_ROWS") == "1" and pol in FULL:
+            for e in above:
+                for k, v in enumerate("xszy"):
+                    ROWS[f"{pol}/{seed}/{int(e)}/{v}"] = got[k][e].copy()
         cols[pol] = {"max_err": float(errs[:, :4].max()), "max_u0_rel": float(errs[:, 4].max()),
                      "n_above": int(len(above)),
                      "above": [[int(e)] + [float(f"{v:.4g}") for v in errs[e]] for e in above[:cap]],
@@ -272,6 +281,8 @@ def main():
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with gzip.open(out, "wt") as fh:
         json.dump({"summary": summary, "cases": cases}, fh)
+    if ROWS:
+        np.savez_compressed(out.replace(".json.gz", "") + ".rows.npz", **ROWS)
     print(json.dumps(summary))
     return 0
 
