@@ -207,12 +207,8 @@ __device__ __forceinline__ void gj_pivot_swp(double (&Sr)[12], double& sc, doubl
     Sr[K] = t;
     pivot_finish<K>(Sr[K], sc, id);
     pivot_zero<K + 1>(Sr[K + 1]);
-#ifdef SRBD_RCP_CUBIC
     const double e = fma(-pk, y, 1.0);
-    const double idn = fma(y, fma(e, e, e), y);
-#else
-    const double idn = fma(y, fma(-pk, y, 1.0), y);  // rcp3's Newton step
-#endif
+    const double idn = SRBD_RCP_NEWTON ? fma(y, e, y) : fma(y, fma(e, e, e), y);  // rcp3's step
     gj_pivot_swp<K + 1>(Sr, sc, idn, Sr[K + 1] * idn);
   } else {
     pivot_update(Sr, t, K);

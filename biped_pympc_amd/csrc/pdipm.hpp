@@ -182,8 +182,8 @@ __device__ inline void sweep_inverse(double (&a)[n * (n + 1) / 2]) {
 // solve must keep the stiff direction: Phi_f reaches cond ~1e12 as the barrier sharpens, and an
 // explicit inverse applied to a vector loses the component along G_i (error ~cond x that of a stable
 // solve) that Lambda ~ W then multiplies into dz (scripts/stiff_dz_emu.py).
-// kRcp: pivot reciprocals by rcp3 (~2^-46 relative; the register kernels' hot loop) instead of IEEE
-// division (the general and LDS-resident kernels, the accuracy baseline).
+// kRcp: pivot reciprocals by rcp3 (v_rcp_f64 + the cubic step, correctly rounded; the register kernels'
+// hot loop) instead of IEEE division (the general and LDS-resident kernels).
 template <int n, bool kRcp = false>
 __device__ inline void ldlt_factor(double (&a)[n * (n + 1) / 2]) {
   double d[n];

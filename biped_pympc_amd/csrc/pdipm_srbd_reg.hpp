@@ -1627,7 +1627,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
-    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (5e3 in mode 0), e.g. an s
+    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (1e4 in mode 0), e.g. an s
     // at or near its 1e-8 clamp (sparse_pdipm_solver.py:520) -- is where the reduced solve's affine
     // ds, dz lose digits; their error enters sigma and the corrector, and the trajectory drifts from the
     // reference's (profiles/r02/refinement_4row.txt; round 5: scripts/parity_fuzz.py found iterates at

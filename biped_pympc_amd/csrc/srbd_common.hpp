@@ -239,19 +239,22 @@ __host__ __device__ inline int a_pidx(const Tables& t, int N, int i, int r) {
 #define PROF_NOW() 0ull
 #endif
 
-// 1/d: v_rcp_f64 (~2^-24 relative) refined by one Newton step y (1 + e), e = 1 - d y: relative
-// error ~2^-46 (not always correctly rounded), two dependent FMAs. The cubic step y (1 + e + e^2)
-// (-DSRBD_RCP_CUBIC) is correctly rounded on 4M log-uniform samples (scripts/microbench_fp64.hip)
-// for one FMA more; the Newton step measured -0.6 % (N = 10) / -1.4 % (N = 20) on the fused step
-// with oracle parity unchanged in magnitude (profiles/r01/rcp_variants.txt)
+// 1/d: v_rcp_f64 (~2^-24 relative) refined by the cubic step y (1 + e + e^2), e = 1 - d y: correctly
+// rounded on 4M log-uniform samples (scripts/microbench_fp64.hip), i.e. the reference's IEEE 1 / d, for
+// three dependent FMAs. Round 6: the Newton step y (1 + e) alone (~2^-46 relative, -DSRBD_RCP_NEWTON),
+// the product's choice since round 1 (profiles/r01/rcp_variants.txt: -0.6 % at N = 10, parity magnitudes
+// in the tests unchanged), left the parity campaign's register kernels at 7 / 11 failing cases of 6657
+// per sequence where correctly rounded reciprocals give 3 / 2 -- through the solves' pivots (the 12x12
+// chain blocks, the 4x4 foot blocks): correctly rounded W = z / s, 1 / s and step-length ratios alone left
+// the counts unchanged (profiles/r06/rcp_*/).
+#ifndef SRBD_RCP_NEWTON
+#define SRBD_RCP_NEWTON 0
+#endif
 __device__ __forceinline__ double rcp3(double d) {
   const double y = __builtin_amdgcn_rcp(d);
   const double e = fma(-d, y, 1.0);
-#ifdef SRBD_RCP_CUBIC
+  if constexpr (SRBD_RCP_NEWTON) return fma(y, e, y);
   return fma(y, fma(e, e, e), y);
-#else
-  return fma(y, e, y);
-#endif
 }
 
 // ------------------------------------------------------------------ wave64 reductions ----

@@ -8,6 +8,7 @@
 #   ccs      the _ccs-sequence campaign, $CCS_SECONDS (420) s, the same policies
 #   bench    the default bench line and the driver-form run
 #   ab       alternating bench runs against $AB_LIB (default ab/libsrbd_mpc_r05.so), N = 10 and 20
+#   fixture  the fuzz-regression fixture under each policy of $FIXTURE_POLICIES (scripts/fixture_policies.py)
 #   seeds    chosen campaign cases ($SEEDS_DEFAULT, $SEEDS_CCS) under each library of $SEEDS_LIBS
 #   profile  rocprofv3 kernel stats of the bench command, PMC traffic and SQ passes, the configs, smoke,
 #            the two-rank launcher rehearsal on one device over gloo
@@ -51,6 +52,9 @@ for step in ${STEPS:-tests}; do
         done
       done
       ls $O/seeds_* ;;
+    fixture)
+      timeout -k 10 300 python -u scripts/fixture_policies.py ${FIXTURE_POLICIES:-adaptive strict} > $O/fixture_policies.jsonl 2> $O/fixture.err || { tail -30 $O/fixture.err; exit 1; }
+      cut -c1-400 $O/fixture_policies.jsonl ;;
     bench)
       timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
       timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $O/bench_driver_form.json 2> $O/bench_driver_form.err || exit 1
