@@ -654,10 +654,11 @@ struct SolverCtx {
 
   // One step of iterative refinement of a direction against the full KKT from the residuals of all
   // four rows (pdipm_srbd.hpp FastCtx::refine_rhs has the scheme, pdipm_srbd_reg.hpp RegCtx::refine_rhs
-  // the derivation): step 0 per inequality row q = D^-1 (e2 - W e3), VV += q, RS -= e3, DZ += q; then
+  // the derivation): step 0 per inequality row q = D^-1 (e2 - W e3), DZ += q, DS += e3 + delta q (the
+  // parts of the correction of dz, ds that do not depend on the correction of dx); then
   // RX <- -(e1 - G^T q) (G^T over the updated DZ), RE <- -e4; dx and dy saved to the output rows for
-  // solve(true). RX, RE, RS are overwritten (the caller restores them with residuals() after
-  // refining the affine direction).
+  // solve(true), which adds Lambda G c_x to dz and (delta Lambda - 1) G c_x to ds. RX, RE are
+  // overwritten (the caller restores them with residuals() after refining the affine direction).
   __device__ void refine_rhs() {
     for (int q = lane; q < m; q += nt) {  // step 0 (rows 2 and 3)
       const int i = q / 16, k = q % 16;
@@ -666,8 +667,7 @@ struct SolverCtx {
       const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
       const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
       const double qc = DI[q] * (e2 - WD[q] * e3);
-      VV[q] = VV[q] + qc;
-      RS[q] = RS[q] - e3;
+      DS[q] = DS[q] + (e3 + kDelta * qc);
       DZ[q] = DZ[q] + qc;
     }
     __syncthreads();
@@ -719,9 +719,11 @@ struct SolverCtx {
   // ------------------------------------------------------------------------- solve ----
   // Solves K [dx; ds; dz; dy] = [-RX; R2; -RS; -RE] with the current factors.
   // Result: dx -> TV, ds -> DS, dz -> DZ, dy -> DY.
-  // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (VV, RS from refine_rhs's
-  // step 0 carry rows 2 and 3), then dx = saved + correction before dz, ds are formed; DY is the
-  // correction.
+  // ref: the refinement solve -- rhs [-RX; 0; 0; -RE] for the correction (refine_rhs's step 0 carried
+  // rows 2 and 3 into DZ, DS), dx = saved + correction; DY is the correction. dz and ds move by the
+  // correction's own Lambda G c_x: re-forming them from the whole dx, dz = VV + Lambda G dx, would
+  // round G dx at eps |G| |dx| and multiply that by Lambda = W / (1 + delta W) -- at z / s = 6e5 it
+  // left dz 1e-9 off the exact answer after the refinement (scripts/extended_precision_check.py).
   __device__ void solve(bool ref = false) {
     if (!ref)
       for (int q = lane; q < m; q += nt) VV[q] = DI[q] * (R2[q] + WD[q] * RS[q]);  // D^-1 (r2 - W r3)
@@ -912,7 +914,9 @@ struct SolverCtx {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           const int o = b + T->foot_col[f][a];
-          TV[o] = ref ? xsg[o] + (TV[o] - tv[a]) : TV[o] - tv[a];
+          const double cv = TV[o] - tv[a];
+          if (ref) R1T[o] = cv;  // the correction of the foot columns (R1T is dead there)
+          TV[o] = ref ? xsg[o] + cv : cv;
         }
       } else {
         const double p6 = phiu(i, 6), p9 = phiu(i, 9), e6 = E6(i), e9 = E9(i);
@@ -935,10 +939,17 @@ struct SolverCtx {
     for (int q = lane; q < m; q += nt) {
       const int i = q / 16, k = q % 16;
       double gd = 0.0;
-      gd = grow_dot(i, k, TV + 12 * N + 12 * i, gd);
-      const double dz = VV[q] + DI[q] * WD[q] * gd;
-      DZ[q] = dz;
-      DS[q] = -RS[q] - gd + kDelta * dz;
+      if (ref) {  // G touches the foot columns only
+        gd = grow_dot(i, k, R1T + 12 * N + 12 * i, gd);
+        const double lg = DI[q] * WD[q] * gd;
+        DZ[q] = DZ[q] + lg;
+        DS[q] = DS[q] + (kDelta * lg - gd);
+      } else {
+        gd = grow_dot(i, k, TV + 12 * N + 12 * i, gd);
+        const double dz = VV[q] + DI[q] * WD[q] * gd;
+        DZ[q] = dz;
+        DS[q] = -RS[q] - gd + kDelta * dz;
+      }
     }
     __syncthreads();
     PROF_ADD_CTX((*this), 6);

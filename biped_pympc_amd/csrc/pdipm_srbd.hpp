@@ -301,11 +301,11 @@ struct FastCtx {
   // profiles/r02/refinement_4row.txt):
   //   e1 = -r_x - (H + beta) dx - G^T dz - A^T dy,   e2 = r2 - (W ds + dz),
   //   e3 = -r_s - (G dx + ds - delta dz),           e4 = -r_e - (A dx - delta dy).
-  // Step 0, per inequality row: q = D^-1 (e2 - W e3); VV += q and r_s -= e3, so solve(2)'s
-  // re-formation dz = VV + Lambda G dx, ds = -r_s - G dx + delta dz yields dz + c_z, ds + c_s; dz += q
-  // so that G^T (dz + q) folds the reduced right-hand side e1 - G^T q into row 1. Then
+  // Step 0, per inequality row: q = D^-1 (e2 - W e3); dz += q and ds += e3 + delta q -- the parts of
+  // c_z, c_s that do not depend on c_x (solve(2) adds Lambda G c_x and (delta Lambda - 1) G c_x) --
+  // and G^T (dz + q) folds the reduced right-hand side e1 - G^T q into row 1. Then
   // RX <- -(e1 - G^T q), RE <- -e4, dx and dy saved to the output rows for solve(2).
-  // RX, RE and RS are overwritten: the caller restores them (residuals()) when the direction refined
+  // RX and RE are overwritten: the caller restores them (residuals()) when the direction refined
   // is the affine one and the combined solve still needs them.
   __device__ void refine_rhs() {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
@@ -315,8 +315,7 @@ struct FastCtx {
       const double e3 = -RS[q] - ((gd + DS[q]) - kDelta * DZ[q]);
       const double e2 = R2[q] - (WD[q] * DS[q] + DZ[q]);
       const double qc = DI[q] * (e2 - WD[q] * e3);
-      VV[q] = VV[q] + qc;
-      RS[q] = RS[q] - e3;
+      DS[q] = DS[q] + (e3 + kDelta * qc);
       DZ[q] = DZ[q] + qc;
     }
     __syncthreads();
@@ -361,7 +360,11 @@ struct FastCtx {
 
   // ------------------------------------------------------------------------ solve ----
   // mode 0: affine rhs r2 = -(S^-1 (s o z)); mode 1: combined r2 = affine - S^-1 (s o z + ds o dz - smu);
-  // mode 2: the refinement solve (rhs from refine_rhs, VV from refine_rhs's step 0, dx = saved + correction)
+  // mode 2: the refinement solve (rhs from refine_rhs, dx = saved + correction; dz, ds move by the
+  // correction's own Lambda G c_x: re-formed from the whole dx, dz = VV + Lambda G dx rounds G dx at
+  // eps |G| |dx| and multiplies that by Lambda = W / (1 + delta W), which at z / s = 6e5 left dz 1e-9
+  // off the exact answer after the refinement, scripts/extended_precision_check.py; the correction of
+  // the u columns goes to VV, dead after refine_rhs)
   __device__ void solve(int mode, double smu) {
     const int N = NT > 0 ? NT : N_, nz = 24 * N, m = 16 * N, p = 14 * N;
     (void)nz; (void)m; (void)p;
@@ -533,7 +536,9 @@ struct FastCtx {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           const int o = b + c_tab.foot_col[f][a];
-          TV[o] = ref ? xsg[o] + (TV[o] - tv[a]) : TV[o] - tv[a];
+          const double cv = TV[o] - tv[a];
+          if (ref) VV[12 * i + c_tab.foot_col[f][a]] = cv;
+          TV[o] = ref ? xsg[o] + cv : cv;
         }
       } else {
         const double r4a = -RE[12 * N + 2 * i], r4b = -RE[12 * N + 2 * i + 1];
@@ -543,6 +548,12 @@ struct FastCtx {
         TV[b + 9] = ref ? xsg[b + 9] + (TV[b + 9] - SG[2] * a9) : TV[b + 9] - SG[2] * a9;
         TV[b + 8] = ref ? xsg[b + 8] + (TV[b + 8] - SG[1] * a8) : TV[b + 8] - SG[1] * a8;
         TV[b + 11] = ref ? xsg[b + 11] + (TV[b + 11] - SG[3] * a11) : TV[b + 11] - SG[3] * a11;
+        if (ref) {  // no G entries in these columns: zeros for the dense G rows below
+          VV[12 * i + 6] = 0.0;
+          VV[12 * i + 8] = 0.0;
+          VV[12 * i + 9] = 0.0;
+          VV[12 * i + 11] = 0.0;
+        }
         const double rho6 = -RX[b + 6] - a6, rho9 = -RX[b + 9] - a9;  // no G entries in cols 6, 9
         DY[12 * N + 2 * i] = (SG[6] * rho6 - SG[4] * r4a) / (SG[4] * kDelta + SG[6] * SG[6]);
         DY[12 * N + 2 * i + 1] = (SG[7] * rho9 - SG[5] * r4b) / (SG[5] * kDelta + SG[7] * SG[7]);
@@ -552,10 +563,17 @@ struct FastCtx {
     __syncthreads();
     for (int q = lane; q < m; q += 64) {  // dz, ds
       const int i = q / 16, k = q % 16;
-      const double gd = dotrow12(Gd + 12 * k, TV + 12 * N + 12 * i);
-      const double dz = VV[q] + DI[q] * WD[q] * gd;
-      DZ[q] = dz;
-      DS[q] = -RS[q] - gd + kDelta * dz;
+      if (ref) {
+        const double gd = dotrow12(Gd + 12 * k, VV + 12 * i);
+        const double lg = DI[q] * WD[q] * gd;
+        DZ[q] = DZ[q] + lg;
+        DS[q] = DS[q] + (kDelta * lg - gd);
+      } else {
+        const double gd = dotrow12(Gd + 12 * k, TV + 12 * N + 12 * i);
+        const double dz = VV[q] + DI[q] * WD[q] * gd;
+        DZ[q] = dz;
+        DS[q] = -RS[q] - gd + kDelta * dz;
+      }
     }
     __syncthreads();
     PROF_ADD(3);
