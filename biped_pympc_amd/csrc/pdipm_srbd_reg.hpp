@@ -455,6 +455,7 @@ struct RegCtx {
   __device__ double hval(int t, int q) const { return (kFReg || t < SI - 1) ? hvr[t] : hg()[q]; }
   // ph: this foot-task lane's LDL^T factors of its foot block Phi_f (foot_inverse, phi_solve)
   double s[SI], z[SI], wd[SI], di[SI], ds[SI], dz[SI], rs[SI], re[SE], rxx[SX], ph[10];
+  double e3r[SI];  // the affine refinement's row-3 residuals (degenerate iterations only)
   PROF_DECL
 
   __device__ double* at(int off) const { return L + off; }
@@ -895,17 +896,13 @@ struct RegCtx {
   //        diagonal with no G, so their row-1 residual is rounding only)
   //   e2 = r2 - (W ds + dz),   e3 = -r_s - (G dx + ds - delta dz),   e4 = -r_e - (A dx - delta dy)
   // is taken through the same elimination, block Gauss-Seidel:
-  //   0. q = D^-1 (e2 - W e3) per inequality row; dz += q, ds += e3 + delta q (the parts of c_z, c_s
-  //      that do not depend on c_x);
+  //   0. q = D^-1 (e2 - W e3) per inequality row; VV += q and r_s -= e3, so that solve_finish<true>'s
+  //      re-formation dz = VV + Lambda G dx, ds = -r_s - G dx + delta dz yields dz + c_z, ds + c_s;
   //   1. dx_f += Phi_f^-1 (e1 - G^T q) on the foot columns (G^T (dz + q) in one pass over Z);
   //   2. rho = A_dyn dx + r_e - delta dy = A t_c - e4 (the x-moment rows are eliminated exactly by
   //      their 2x2 blocks);
   //   3. one more chain solve S c = rho; dy += c, dx -= Phi~^-1 A^T c (solve_finish<true>, which
-  //      leaves row 1 as step 1 made it); dz += Lambda G c_x, ds += (delta Lambda - 1) G c_x with the
-  //      foot columns' correction c_x (steps 1 and 3) kept in LDS. Re-forming dz = VV + Lambda G dx from
-  //      the whole dx instead (rounds 1-6) rounds G dx at eps |G| |dx| and multiplies that by
-  //      Lambda = W / (1 + delta W): at z / s = 6e5 it left dz 1e-9 off the exact answer after the
-  //      refinement, where the additive form reaches ~1e-15 (scripts/extended_precision_check.py).
+  //      leaves row 1 as step 1 made it) and dz, ds re-formed from dx.
   // On the SURVEY workloads this sits at the dense-LU-vs-oracle floor over 512 envs per case at
   // K = 1/10/20 (profiles/r02/refinement_variants.txt). dy is parked in RXu (r_x's u part is dead
   // once step 1 has read it) while QV carries rho and then c.
@@ -919,38 +916,35 @@ struct RegCtx {
     if (kPark) DYs[sink(q.valid, q.e, Lo::RXu)] = dy;
     QV[e] = (v + re[t]) - kDelta * dy;
   }
-  // kAff: the affine (predictor) direction at a degenerate iterate (see the main loop): step 0 runs
-  // here (the combined direction's in its solve_finish), and dy is not parked (RXu still feeds the
-  // combined solve)
+  // kAff: the affine (predictor) direction at a degenerate iterate (see the main loop): r_s stays
+  // (the combined solve needs it), e3 goes to Z for solve_finish<true, true>, and dy is not parked
+  // (RXu still feeds the combined solve)
   // row1 = false (refinement policy 3): the dual rows only -- no KKT row-1 foot correction
   template <bool kAff = false>
   SRBD_PHASE_ATTR __device__ void refine_rhs(bool row1 = true) {
     const int lane = fresh_lane();
     const double *Mc = at(Lo::Mc), *Nd = at(Lo::Nd), *Pd = at(Lo::Pd), *Gf = at(Lo::Gf), *Hu = at(Lo::Hu);
-    double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z), *VC = at(Lo::VV);
+    double *TV = at(Lo::TV), *QV = at(Lo::QV), *DYs = at(Lo::RXu), *Zd = at(Lo::Z);
     if constexpr (kAff) {  // step 0 for the affine direction (the combined one ran it in its finish)
+      double *VV = at(Lo::VV);
 #pragma unroll
       for (int t = 0; t < SI; ++t) {
         const int q = lane + TPB * t;
+        e3r[t] = 0.0;
         if (RegCtx<N>::full_slot(t, m) || q < m) {
           const int i = q >> 4, k = q & 15;
           const double gd = grow4(Gf, k, TV + nx + m24(i, 12));
           const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
           const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
           const double qc = di[t] * (e2 - wd[t] * e3);
-          VC[q] = ds[t] + (e3 + kDelta * qc);  // ds + e3 + delta q in VV, dz + q in Z (dz, ds free)
+          VV[q] = VV[q] + qc;
+          e3r[t] = e3;
           Zd[q] = dz[t] + qc;
         }
       }
     }
     qp_sync<TPB>();  // (the combined direction's step 0 ran in its solve_finish, kStep0 = 1)
     const int fl = lane;
-    if (!row1 && (unsigned)fl < 2u * N) {  // no row-1 correction: c_x starts at 0 (VC, see above)
-      const int b = 12 * (fl >> 1);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) VC[b + foot_colj(fl & 1, a)] = 0.0;
-    }
-    double c[4];  // the foot columns' c_x: VV (combined direction) or, after rho, TV's x part (affine)
     if (row1 && (unsigned)fl < 2u * N) {  // KKT row 1 on the foot columns: dx_f += Phi_f^-1 e1_f
       const int i = fl >> 1, f = fl & 1, b = 12 * i;
       const double* zf = Zd + 16 * i + 8 * f;
@@ -972,7 +966,7 @@ struct RegCtx {
         }
         gt[2] = gz0 + gz1;
       }
-      double e1[4];
+      double e1[4], c[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         const int j = foot_colj(f, a);
@@ -981,22 +975,16 @@ struct RegCtx {
       }
       phi_solve(fl, e1, c);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        TV[nx + b + foot_colj(f, a)] += c[a];
-        if (!kAff) VC[b + foot_colj(f, a)] = c[a];  // (VV is dead after the combined step 0)
-      }
+      for (int a = 0; a < 4; ++a) TV[nx + b + foot_colj(f, a)] += c[a];
     }
     qp_sync<TPB>();
+    if (kAff) {  // Z is dead from here on: it keeps e3 for solve_finish<true, true>
+#pragma unroll
+      for (int t = 0; t < SI; ++t)
+        if (full_slot(t, m) || lane + TPB * t < m) Zd[lane + TPB * t] = e3r[t];
+    }
     rho_slot<0, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
     rho_slot<1, !kAff>(TV, Mc, Pd, Nd, QV, DYs);
-    if (kAff) {  // TV's x part is dead once rho is formed (the affine finish skips the x columns)
-      qp_sync<TPB>();
-      if ((unsigned)fl < 2u * N) {
-        const int b = 12 * (fl >> 1);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) TV[b + foot_colj(fl & 1, a)] = c[a];
-      }
-    }
     qp_sync<TPB>();
     PROF_ADD(6);
   }
@@ -1167,16 +1155,15 @@ struct RegCtx {
   }
 
   // kRefine: the refinement step -- TV holds dx and QV the dual correction c, so the same updates
-  // give dx - Phi~^-1 A^T c; the x-moment duals move by their 2x2 formula's increment, and dz, ds by
-  // Lambda G c_x, (delta Lambda - 1) G c_x of the foot columns' correction c_x (refine_rhs: in VV for the
-  // combined direction, in TV's x part for the affine one).
+  // give dx - Phi~^-1 A^T c; the x-moment duals move by their 2x2 formula's increment, and dz, ds are
+  // re-formed from the refined dx (with the combined solve's VV, r_s).
   // kAffine: the affine (predictor) direction, of which only ds and dz are consumed (step lengths,
   // mu_aff and the corrector's ds o dz, sparse_pdipm_solver.py:484-490): G touches only the foot
   // columns, so dx is finished on those alone (no x columns, no scalar columns, no x-moment duals).
   // kStep0: refine_rhs's step 0 for the combined direction fused into the row loop, where dz, ds,
-  // G dx and VV are at hand -- e2, e3, q = D^-1 (e2 - W e3); Z = dz + q (also for G^T (dz + q)),
-  // r_s = ds + e3 + delta q (step0 false: skipped at run time -- an iteration whose combined direction
-  // the refinement policy leaves unrefined or refines in the dual rows only)
+  // G dx and VV are at hand -- e2, e3, q = D^-1 (e2 - W e3); VV += q, Z = dz + q for G^T (dz + q),
+  // r_s -= e3 (step0 false: skipped at run time -- an iteration whose combined direction the refinement
+  // policy leaves unrefined or refines in the dual rows only)
   template <bool kRefine = false, bool kAffine = false, bool kStep0 = false>
   SRBD_PHASE_ATTR __device__ void solve_finish(bool step0 = true) {
     const int lane = fresh_lane();
@@ -1211,7 +1198,6 @@ struct RegCtx {
         for (int a = 0; a < 4; ++a) {
           const int o = b + foot_colj(f, a);
           TV[o] = TV[o] - tv[a];
-          if constexpr (kRefine) (kAffine ? TV : VV)[o - nx] -= tv[a];
         }
       } else {
         const double r4a = kRefine ? 0.0 : -REm[2 * i], r4b = kRefine ? 0.0 : -REm[2 * i + 1];
@@ -1237,28 +1223,20 @@ struct RegCtx {
       const int q = lane + TPB * t;
       if (RegCtx<N>::full_slot(t, m) || q < m) {
         const int i = q >> 4, k = q & 15;
-        if constexpr (kRefine) {
-          const double gd = grow4(Gf, k, (kAffine ? TV : VV) + m24(i, 12));
-          const double lg = di[t] * wd[t] * gd;
-          // dz + q from Z, ds + e3 + delta q from VV (affine step 0) or r_s (combined: dead until the
-          // next iteration's residuals), so that dz, ds hold no registers across the chain solve
-          dz[t] = at(Lo::Z)[q] + lg;
-          ds[t] = (kAffine ? VV[q] : rs[t]) + (kDelta * lg - gd);
-        } else {
-          const double gd = grow4(Gf, k, TV + nx + m24(i, 12));
-          dz[t] = VV[q] + di[t] * wd[t] * gd;
-          ds[t] = -rs[t] - gd + kDelta * dz[t];
-          if (kStep0 && step0) {
-            double* Zd = at(Lo::Z);
-            const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
-            const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
-            const double qc = di[t] * (e2 - wd[t] * e3);
-            rs[t] = ds[t] + (e3 + kDelta * qc);
-            Zd[q] = dz[t] + qc;
-          } else if (kStep0) {  // refined in the dual rows only (diagnostic builds): no step 0
-            rs[t] = ds[t];
-            at(Lo::Z)[q] = dz[t];
-          }
+        const double gd = grow4(Gf, k, TV + nx + m24(i, 12));
+        const double vq = VV[q];
+        dz[t] = vq + di[t] * wd[t] * gd;
+        // the affine refinement keeps r_s and parks its row-3 residual e3 in Z (refine_rhs<true>)
+        const double r3 = (kRefine && kAffine) ? at(Lo::Z)[q] - rs[t] : -rs[t];
+        ds[t] = r3 - gd + kDelta * dz[t];
+        if (kStep0 && step0) {
+          double* Zd = at(Lo::Z);
+          const double e3 = -rs[t] - ((gd + ds[t]) - kDelta * dz[t]);
+          const double e2 = Zd[q] - (wd[t] * ds[t] + dz[t]);  // r2 parked in Z by solve_rhs
+          const double qc = di[t] * (e2 - wd[t] * e3);
+          VV[q] = vq + qc;
+          rs[t] = rs[t] - e3;
+          Zd[q] = dz[t] + qc;
         }
       }
     }
@@ -1649,7 +1627,7 @@ __device__ __forceinline__ void reg_kernel_body(const SolverArgs& args, const Fu
     }
     double mu = C.residuals(it == 0);
     if (it > 0) mu = mu_new;
-    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (5e3 in mode 0), e.g. an s
+    // An ill-conditioned iterate -- some row with W = z / s >= refine_w (1e4 in mode 0), e.g. an s
     // at or near its 1e-8 clamp (sparse_pdipm_solver.py:520) -- is where the reduced solve's affine
     // ds, dz lose digits; their error enters sigma and the corrector, and the trajectory drifts from the
     // reference's (profiles/r02/refinement_4row.txt; round 5: scripts/parity_fuzz.py found iterates at

@@ -87,11 +87,10 @@ struct RefinePolicy {
   double w = 0.0;
 };
 // mode 0's policy: the predictor at a solve's initial iterate (all z = 1) and in every iteration with
-// z / s >= 5e3 in some row (round 6, DESIGN.md 3.3: with correctly rounded reciprocals and the additive
-// refinement update, 23 -> 3 failing _ccs-campaign cases of 6657 for +1.4 % at N = 10; at 1e4 the
-// fuzz-regression fixture's env seed 50690 / 61 leaves its u0 bound)
+// z / s >= 1e4 in some row (round 6, DESIGN.md 3.3: with correctly rounded reciprocals, about round 5's
+// N = 10 time for 23 -> 4 failing _ccs-campaign cases of 6657)
 constexpr int kDefaultRefineFlags = SRBD_REFINE_AFFINE_AT_INIT;
-constexpr double kDefaultRefineW = 5e3;
+constexpr double kDefaultRefineW = 1e4;
 srbd::PerDevice<RefinePolicy> g_refinement;
 int refinement_mode() {
   const RefinePolicy* p = g_refinement.at(current_device());

@@ -138,13 +138,13 @@ int srbd_get_solver_path(void);
  * device like the solver path. Every Newton iteration refines the combined direction once against the
  * full KKT; the affine (predictor) direction, whose ds / dz set sigma and the corrector, is refined
  * 0 = (default) at the iterate a solve starts from (every dual z at its initial 1: the cold start's Newton
- *     step is the largest) and in iterations with an ill-conditioned iterate (some row with z / s >= 5e3
+ *     step is the largest) and in iterations with an ill-conditioned iterate (some row with z / s >= 1e4
  *     or an s at its 1e-8 clamp) -- where an unrefined predictor lets the trajectory drift from the
- *     reference's; 1.4 % more time at N = 10 than round 5's mode 0 (predictor at z / s >= 1e3 only);
+ *     reference's; about the time at N = 10 of round 5's mode 0 (predictor at z / s >= 1e3 only);
  * 1 = in every iteration (as the LDS-resident and general kernels always do), ~15 % more time at N = 10.
  * scripts/parity_fuzz.py + scripts/parity_floor.py, every env above the tolerance floor-checked, 6657 cases
- * of each sequence: mode 0 fails 3 (_ccs entry included) and 1 (default) cases, mode 1 none,
- * round 5's mode 0 23 and 26 -- a case fails when an env sits more than 4x its FP64 floor (the
+ * of each sequence: mode 0 fails a few register-kernel warm starts, mode 1 none (DESIGN.md 3.3 has the
+ * counts), round 5's mode 0 23 and 26 -- a case fails when an env sits more than 4x its FP64 floor (the
  * larger distance of the AMD-ordered LDL^T and of dense LU from the checker) beyond the K tolerance; no env
  * of either mode is over 1e-4 relative in x or u0 beyond that (profiles/r06/). Returns 0, or
  * an error for another mode. */
@@ -159,7 +159,7 @@ int srbd_get_refinement(void);
  * initial iterate of the GPU caller's and of the _ccs init), SRBD_REFINE_AFFINE_FIRST(k) /
  * SRBD_REFINE_AFFINE_LAST(k) (in the first / last k iterations of a call -- position-based: chained calls
  * then no longer equal one long call); w: the affine vote's W = z / s threshold (w <= 0: no W vote; an s
- * at its clamp always votes). Mode 0 is SRBD_REFINE_AFFINE_AT_INIT with w = 5e3, mode 1
+ * at its clamp always votes). Mode 0 is SRBD_REFINE_AFFINE_AT_INIT with w = 1e4, mode 1
  * SRBD_REFINE_AFFINE_ALL. The
  * combined direction is refined in every iteration whatever the policy. srbd_set_refinement(mode)
  * returns to a mode. Returns 0, or an error for unknown bits or a NaN threshold. */

@@ -53,14 +53,14 @@ _F = _native.refine_affine_first
 _L = _native.refine_affine_last
 # name -> ("mode", srbd_set_refinement mode) or (srbd_set_refinement_policy flags, W threshold[, alpha])
 POLICIES = {
-    "adaptive": ("mode", 0),            # the default: affine refined at the initial iterate (all z = 1), W >= 5e3, clamp
+    "adaptive": ("mode", 0),            # the default: affine refined at the initial iterate (all z = 1), W >= 1e4, clamp
     "strict": ("mode", 1),              # the affine direction refined in every iteration
     "w1e3": (0, 1e3),                   # round 5's mode 0: W >= 1e3 / clamp only
     "init_w1e3": (2, 1e3),
     "init_w2e3": (2, 2e3),
     "init_w3e3": (2, 3e3),
-    "init_w5e3": (2, 5e3),              # = mode 0 (final build)
-    "init_w1e4": (2, 1e4),              # = mode 0 at build ff0f76fa
+    "init_w5e3": (2, 5e3),
+    "init_w1e4": (2, 1e4),              # = mode 0 since round 6
     "init_w3e4": (2, 3e4),
     "init_only": (2, 0.0),              # the initial-iterate vote alone (w <= 0: no W vote; clamps still vote)
     "w5e3": (0, 5e3),

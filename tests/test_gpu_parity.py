@@ -644,7 +644,7 @@ def test_refinement_mode_is_per_call_and_exact():
 @pytest.mark.parametrize("N", [10, 20, 5])
 def test_refinement_policy_words(N):
     """srbd_set_refinement_policy: the word of mode 0 (the predictor at the initial iterate, all z = 1, + the
-    W >= 5e3 vote) and of mode 1 (every iteration) reproduce the modes bit for bit on the fused step and the
+    W >= 1e4 vote) and of mode 1 (every iteration) reproduce the modes bit for bit on the fused step and the
     CCS solver; round 5's mode 0 (the W vote alone) differs from today's and stays within the tolerance, and
     so does a position-based word (the first iteration of every call); unknown bits and a NaN threshold are
     refused; leaving the context returns to mode 0."""
@@ -663,7 +663,7 @@ def test_refinement_policy_words(N):
     mode0 = both()
     with _native.refinement("every_iteration"):
         mode1 = both()
-    with _native.refinement_policy(_native.REFINE_AFFINE_AT_INIT, 5e3):
+    with _native.refinement_policy(_native.REFINE_AFFINE_AT_INIT, 1e4):
         assert _native.current_refinement() == 2
         p0 = both()
     with _native.refinement_policy(_native.refine_affine_first(1), 1e3):
